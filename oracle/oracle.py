@@ -1,0 +1,151 @@
+"""ctypes wrapper around oracle/liboth_oracle.so -- TEST INFRASTRUCTURE ONLY.
+
+The CPU restatement of the reference rules engine (othello_oracle.c).  Imported
+by tests/, by __graft_entry__.smoke() and by bench.py's cpu_baseline leg only,
+always as the checker; the product package gymothelloenv_amd never imports it.
+All arrays use the exchange format documented in include/othello_mi355x.h.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboth_oracle.so")
+
+F_SUDDEN_DEATH = 1
+F_DISK_REWARD = 2
+F_AUTO_RESET = 4
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH) or (os.path.getmtime(LIB_PATH) <
+                                            os.path.getmtime(os.path.join(HERE, "othello_oracle.c"))):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.c_void_p
+        i32, u32, u64 = ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64
+        L.oracle_nwords.argtypes = [i32]
+        L.oracle_reset_batch.argtypes = [i32, i32, P, P, P]
+        L.oracle_legal_batch.argtypes = [i32, i32, P, P, P]
+        L.oracle_step_batch.argtypes = [i32, u32, i32, P, P, P, P, P, P]
+        L.oracle_step_batch.restype = i32
+        L.oracle_reset_openings.argtypes = [i32, i32, u64, u32, u64, i32, P, P, P]
+        L.oracle_rollout.argtypes = [i32, u32, i32, i32, u64, u32, u64, i32, i32, P, P, P, P, P, P, P]
+        L.oracle_greedy_batch.argtypes = [i32, i32, P, P, P, P]
+        L.oracle_recompute_legal.argtypes = [i32, i32, P, P, P]
+        L.oracle_observe.argtypes = [i32, i32, P, P, P, P, P, P]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def nwords(n):
+    return (n * n + 63) // 64
+
+
+class State(object):
+    """E boards in the exchange format (numpy, host)."""
+
+    def __init__(self, n, E):
+        W = nwords(n)
+        self.n, self.E, self.W = n, E, W
+        self.boards = np.zeros((E, 2 * W), dtype=np.uint64)
+        self.meta = np.zeros(E, dtype=np.uint16)
+        self.legal = np.zeros((E, W), dtype=np.uint64)
+
+    def copy(self):
+        s = State(self.n, self.E)
+        s.boards[:] = self.boards
+        s.meta[:] = self.meta
+        s.legal[:] = self.legal
+        return s
+
+
+def reset(n, E):
+    s = State(n, E)
+    lib().oracle_reset_batch(n, E, _p(s.boards), _p(s.meta), _p(s.legal))
+    return s
+
+
+def reset_openings(n, E, seed, id_base, ply, initial_rand_steps):
+    s = State(n, E)
+    lib().oracle_reset_openings(n, E, seed, id_base, ply, initial_rand_steps,
+                                _p(s.boards), _p(s.meta), _p(s.legal))
+    return s
+
+
+def legal(n, mover, opp):
+    mover = np.ascontiguousarray(mover, dtype=np.uint64)
+    opp = np.ascontiguousarray(opp, dtype=np.uint64)
+    E = mover.shape[0]
+    out = np.zeros((E, nwords(n)), dtype=np.uint64)
+    lib().oracle_legal_batch(n, E, _p(mover), _p(opp), _p(out))
+    return out
+
+
+def step(s, flags, actions):
+    """In-place step of State s; returns (rewards, dones, n_stepped_while_terminated)."""
+    actions = np.ascontiguousarray(actions, dtype=np.int32)
+    rewards = np.zeros(s.E, dtype=np.int32)
+    dones = np.zeros(s.E, dtype=np.uint8)
+    errs = lib().oracle_step_batch(s.n, flags, s.E, _p(s.boards), _p(s.meta), _p(s.legal),
+                                   _p(actions), _p(rewards), _p(dones))
+    return rewards, dones, errs
+
+
+def rollout(s, flags, policy, plies, seed=0, id_base=0, ply0=0, initial_rand_steps=0, record=True):
+    """In-place rollout; returns (actions, rewards, dones [plies, E] or None, wdl int64[3])."""
+    E = s.E
+    acts = np.zeros((plies, E), dtype=np.int32) if record else None
+    rews = np.zeros((plies, E), dtype=np.int32) if record else None
+    dns = np.zeros((plies, E), dtype=np.uint8) if record else None
+    wdl = np.zeros(3, dtype=np.int64)
+    lib().oracle_rollout(s.n, flags, policy, initial_rand_steps, seed, id_base, ply0, E, plies,
+                         _p(s.boards), _p(s.meta), _p(s.legal), _p(acts), _p(rews), _p(dns), _p(wdl))
+    return acts, rews, dns, wdl
+
+
+def greedy(s):
+    out = np.zeros(s.E, dtype=np.int32)
+    lib().oracle_greedy_batch(s.n, s.E, _p(s.boards), _p(s.meta), _p(s.legal), _p(out))
+    return out
+
+
+def recompute_legal(s):
+    out = np.zeros_like(s.legal)
+    lib().oracle_recompute_legal(s.n, s.E, _p(s.boards), _p(s.meta), _p(out))
+    return out
+
+
+def observe(s):
+    """(obs int8 (E,N,N), obs2 int8 (E,2,N,N), make_state float32 (E,4,N,N))."""
+    n, E = s.n, s.E
+    obs = np.zeros((E, n, n), dtype=np.int8)
+    obs2 = np.zeros((E, 2, n, n), dtype=np.int8)
+    ms = np.zeros((E, 4, n, n), dtype=np.float32)
+    lib().oracle_observe(n, E, _p(s.boards), _p(s.meta), _p(s.legal), _p(obs), _p(obs2), _p(ms))
+    return obs, obs2, ms
+
+
+def meta_from(turn, terminated=False, winner=0, rand_left=0):
+    """Pack reference-style (player_turn, terminated, winner) into the meta word."""
+    m = np.asarray(turn) == 1
+    m = m.astype(np.uint16)
+    m |= (np.asarray(terminated).astype(np.uint16) << 1)
+    w = np.asarray(winner)
+    m |= (np.where(w == 1, 1, np.where(w == -1, 2, 0)).astype(np.uint16) << 2)
+    m |= (np.asarray(rand_left).astype(np.uint16) << 8)
+    return m.astype(np.uint16)

@@ -1,0 +1,313 @@
+"""Generate the golden fixtures under tests/golden/ from the reference itself.
+
+Runs ONLY in the build container (the reference tree is not on the GPU box).
+It imports the reference's `othello.py`, `simple_policies.py` and `util.py`
+read-only from /root/reference, with tiny stand-ins for the modules those files
+import but never compute with (gym's `Env`/`spaces`, pyglet, the `ppo` and
+`Rainbow` imports at the top of util.py).  No reference source is copied: the
+fixtures are inputs and outputs only (bitboards, actions, rewards, flags).
+
+Bit convention used in every fixture: square a = row * N + col
+(`othello.py:392-393`), word a // 64, bit a % 64, W = ceil(N*N / 64) words per
+colour.
+
+    python tests/golden/gen_golden.py        # rewrites tests/golden/*.npz|json
+"""
+import contextlib
+import io
+import json
+import os
+import sys
+import types
+
+import numpy as np
+
+sys.dont_write_bytecode = True
+REF = os.environ.get("OTHELLO_REFERENCE", "/root/reference")
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+SIZES = list(range(4, 17))
+COMBOS = [(sd, dr) for sd in (True, False) for dr in (False, True)]  # (sudden_death, disk_reward)
+
+
+def install_shims():
+    """Stand-ins for modules imported (but not used for arithmetic) by the reference."""
+    gym = types.ModuleType("gym")
+
+    class Env(object):
+        pass
+
+    gym.Env = Env
+    spaces = types.ModuleType("gym.spaces")
+
+    class Discrete(object):
+        def __init__(self, n):
+            self.n = n
+
+    class Box(object):
+        def __init__(self, low, high, shape=None, dtype=None):
+            self.low, self.high, self.shape = low, high, np.shape(low)
+
+    spaces.Discrete, spaces.Box = Discrete, Box
+    gym.spaces = spaces
+    pyglet = types.ModuleType("pyglet")
+    gl = types.ModuleType("pyglet.gl")
+    pyglet.gl = gl
+    ppo = types.ModuleType("ppo")
+    ppo.PPO = object
+    rainbow = types.ModuleType("Rainbow")
+    rainbow_agent = types.ModuleType("Rainbow.agent")
+    rainbow_agent.Agent = object
+    rainbow.agent = rainbow_agent
+    sys.modules.update({"gym": gym, "gym.spaces": spaces, "pyglet": pyglet,
+                        "pyglet.gl": gl, "ppo": ppo, "Rainbow": rainbow,
+                        "Rainbow.agent": rainbow_agent})
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+
+
+def nwords(n):
+    return (n * n + 63) // 64
+
+
+def pack(cells, n):
+    """bool (N*N,) -> (W,) uint64."""
+    w = np.zeros(nwords(n), dtype=np.uint64)
+    for a in np.flatnonzero(cells):
+        w[a // 64] |= np.uint64(1) << np.uint64(a % 64)
+    return w
+
+
+def pack_moves(moves, n):
+    cells = np.zeros(n * n, dtype=bool)
+    cells[list(moves)] = True
+    return pack(cells, n)
+
+
+def board_bits(board, n):
+    flat = np.asarray(board).ravel()
+    return pack(flat == -1, n), pack(flat == 1, n)
+
+
+def snapshot(env, n):
+    b, w = board_bits(env.board_state, n)
+    return b, w, int(env.player_turn), pack_moves(env.possible_moves, n)
+
+
+def gen_trajectories(othello):
+    """Random play (with occasional invalid actions) in all four flag combos."""
+    for n in SIZES:
+        games = 12 if n <= 10 else 4
+        rec = {k: [] for k in ("combo", "game", "ply", "action", "black", "white",
+                               "turn", "legal", "reward", "done", "winner",
+                               "prev_black", "prev_white", "prev_turn", "prev_legal")}
+        starts = []
+        for ci, (sd, dr) in enumerate(COMBOS):
+            for g in range(games):
+                rnd = np.random.RandomState(1000 * n + 100 * ci + g)
+                env = othello.OthelloBaseEnv(board_size=n, sudden_death_on_invalid_move=sd,
+                                             num_disk_as_reward=dr, mute=True)
+                env.reset()
+                b, w, t, lg = snapshot(env, n)
+                starts.append((ci, g, b, w, t, lg))
+                ply = 0
+                done = False
+                p_invalid = 0.02 if sd else 0.06
+                while not done:
+                    if rnd.rand() < p_invalid:
+                        action = int(rnd.randint(-1, n * n + 1))
+                    else:
+                        pm = env.possible_moves
+                        action = int(pm[rnd.randint(0, len(pm))])
+                    pb, pw, pt, pl = snapshot(env, n)
+                    _, reward, done, info = env.step(action)
+                    assert info is None
+                    b, w, t, lg = snapshot(env, n)
+                    for k, v in (("combo", ci), ("game", g), ("ply", ply), ("action", action),
+                                 ("black", b), ("white", w), ("turn", t), ("legal", lg),
+                                 ("reward", int(reward)), ("done", bool(done)),
+                                 ("winner", int(env.winner)), ("prev_black", pb),
+                                 ("prev_white", pw), ("prev_turn", pt), ("prev_legal", pl)):
+                        rec[k].append(v)
+                    ply += 1
+                # stepping a terminated game must raise (othello.py:415-416)
+                try:
+                    env.step(0)
+                    raise AssertionError("reference did not raise after termination")
+                except ValueError:
+                    pass
+        arrays = {k: np.array(v) for k, v in rec.items()}
+        for k in ("black", "white", "legal", "prev_black", "prev_white", "prev_legal"):
+            arrays[k] = arrays[k].astype(np.uint64).reshape(-1, nwords(n))
+        arrays["action"] = arrays["action"].astype(np.int32)
+        arrays["reward"] = arrays["reward"].astype(np.int32)
+        arrays["turn"] = arrays["turn"].astype(np.int8)
+        arrays["prev_turn"] = arrays["prev_turn"].astype(np.int8)
+        arrays["winner"] = arrays["winner"].astype(np.int8)
+        arrays["combo"] = arrays["combo"].astype(np.int8)
+        arrays["combos"] = np.array(COMBOS, dtype=np.int8)
+        arrays["start_black"] = np.array([s[2] for s in starts], dtype=np.uint64)
+        arrays["start_white"] = np.array([s[3] for s in starts], dtype=np.uint64)
+        arrays["start_legal"] = np.array([s[5] for s in starts], dtype=np.uint64)
+        np.savez_compressed(os.path.join(OUT, "traj_N%d.npz" % n), **arrays)
+        print("traj N=%d: %d plies" % (n, len(rec["action"])))
+
+
+def gen_kat(othello):
+    kat = {}
+    for n in SIZES:
+        env = othello.OthelloBaseEnv(board_size=n, mute=True)
+        env.reset()
+        b, w, _, _ = snapshot(env, n)
+        legal0 = list(map(int, env.possible_moves))
+        env.step(legal0[0])
+        kat[str(n)] = {"black": [int(x) for x in b], "white": [int(x) for x in w],
+                       "black_moves": legal0, "white_moves_after_lowest": list(map(int, env.possible_moves)),
+                       "action_space_n": env.action_space.n}
+    # board_size is clamped to >= 4 (othello.py:230)
+    kat["clamp"] = {"requested": 2, "board_size": othello.OthelloBaseEnv(board_size=2, mute=True).board_size}
+    with open(os.path.join(OUT, "kat.json"), "w") as f:
+        json.dump(kat, f, indent=1, sort_keys=True)
+
+
+def gen_greedy(othello, simple_policies, util):
+    """Positions from random play -> reference GreedyPolicy's choice (make_state obs)."""
+    out = {}
+    for n in SIZES:
+        positions = 160 if n <= 8 else (60 if n <= 12 else 25)
+        rnd = np.random.RandomState(7 + n)
+        env = othello.OthelloBaseEnv(board_size=n, mute=True)
+        pol = simple_policies.GreedyPolicy()
+        pol.reset(env)
+        blacks, whites, turns, acts = [], [], [], []
+        while len(acts) < positions:
+            env.reset()
+            done = False
+            while not done and len(acts) < positions:
+                obs = util.make_state(env.get_observation(), env)
+                if rnd.rand() < 0.35:
+                    a = int(pol.get_action(obs))
+                    b, w, t, _ = snapshot(env, n)
+                    blacks.append(b)
+                    whites.append(w)
+                    turns.append(t)
+                    acts.append(a)
+                pm = env.possible_moves
+                _, _, done, _ = env.step(int(pm[rnd.randint(0, len(pm))]))
+        out["N%d_black" % n] = np.array(blacks, dtype=np.uint64)
+        out["N%d_white" % n] = np.array(whites, dtype=np.uint64)
+        out["N%d_turn" % n] = np.array(turns, dtype=np.int8)
+        out["N%d_action" % n] = np.array(acts, dtype=np.int32)
+    np.savez_compressed(os.path.join(OUT, "greedy.npz"), **out)
+
+
+def gen_obs(othello, util):
+    """get_observation (1- and 2-plane) and util.make_state on 6x6 / 8x8 positions."""
+    out = {}
+    for n in (6, 8):
+        rnd = np.random.RandomState(99 + n)
+        blacks, whites, turns, legals, obs1, obs2, ms, nlegal = [], [], [], [], [], [], [], []
+        env = othello.OthelloBaseEnv(board_size=n, mute=True, possible_actions_in_obs=True)
+        env1 = othello.OthelloBaseEnv(board_size=n, mute=True)
+        for g in range(30):
+            env.reset()
+            done = False
+            while not done:
+                o2 = env.get_observation()
+                env1.board_state = env.board_state.copy()
+                env1.player_turn = env.player_turn
+                env1.possible_moves = list(env.possible_moves)
+                o1 = env1.get_observation()
+                st = util.make_state(o1, env1)
+                assert o1.dtype == np.int64 and o2.dtype == np.int64 and o2.shape == (2, n, n)
+                assert st.dtype == np.float64 and set(np.unique(st)) <= {0.0, 1.0}
+                b, w, t, lg = snapshot(env, n)
+                blacks.append(b); whites.append(w); turns.append(t); legals.append(lg)
+                obs1.append(o1.astype(np.int8)); obs2.append(o2.astype(np.int8))
+                ms.append(st.astype(np.uint8)); nlegal.append(len(env.possible_moves))
+                pm = env.possible_moves
+                _, _, done, _ = env.step(int(pm[rnd.randint(0, len(pm))]))
+            # terminal position too (stale possible_moves, turn left on the mover)
+            o2 = env.get_observation()
+            env1.board_state = env.board_state.copy()
+            env1.player_turn = env.player_turn
+            env1.possible_moves = list(env.possible_moves)
+            o1 = env1.get_observation()
+            st = util.make_state(o1, env1)
+            b, w, t, lg = snapshot(env, n)
+            blacks.append(b); whites.append(w); turns.append(t); legals.append(lg)
+            obs1.append(o1.astype(np.int8)); obs2.append(o2.astype(np.int8))
+            ms.append(st.astype(np.uint8)); nlegal.append(len(env.possible_moves))
+        out["N%d_black" % n] = np.array(blacks, dtype=np.uint64)
+        out["N%d_white" % n] = np.array(whites, dtype=np.uint64)
+        out["N%d_turn" % n] = np.array(turns, dtype=np.int8)
+        out["N%d_legal" % n] = np.array(legals, dtype=np.uint64)
+        out["N%d_obs" % n] = np.array(obs1)
+        out["N%d_obs2" % n] = np.array(obs2)
+        out["N%d_make_state" % n] = np.array(ms)
+        out["N%d_nlegal" % n] = np.array(nlegal, dtype=np.int32)
+        print("obs N=%d: %d positions, %d with exactly one legal move" %
+              (n, len(turns), int((np.array(nlegal) == 1).sum())))
+    np.savez_compressed(os.path.join(OUT, "obs.npz"), **out)
+
+
+def enc(obs):
+    """Mover-perspective board (values -1/0/+1) as a string over '-', '0', '+'."""
+    return "".join("-0+"[int(v) + 1] for v in obs.ravel())
+
+
+def gen_wrappers(othello, simple_policies):
+    """OthelloEnv / SimpleOthelloEnv traces driven by seeded RandomPolicy (config 1)."""
+    traces = []
+    quiet = io.StringIO()
+    for cls_name in ("OthelloEnv", "SimpleOthelloEnv"):
+        for protagonist in (1, -1):
+            for init_rand in (0, 10):
+                for disk in (False, True):
+                    if cls_name == "SimpleOthelloEnv" and protagonist == -1:
+                        continue
+                    kw = dict(board_size=8, seed=0, initial_rand_steps=init_rand,
+                              num_disk_as_reward=disk)
+                    if cls_name == "OthelloEnv":
+                        opp = simple_policies.RandomPolicy(seed=1)
+                        env = othello.OthelloEnv(white_policy=opp, black_policy=opp,
+                                                 protagonist=protagonist, **kw)
+                    else:
+                        env = othello.SimpleOthelloEnv(**kw)
+                    me = simple_policies.RandomPolicy(seed=0)
+                    games = []
+                    with contextlib.redirect_stdout(quiet):
+                        for _ in range(6):
+                            obs = env.reset()
+                            me.reset(env)
+                            steps = [{"obs": enc(obs), "turn": int(env.player_turn),
+                                      "moves": list(map(int, env.possible_moves))}]
+                            done = False
+                            while not done:
+                                a = int(me.get_action(obs))
+                                obs, r, done, info = env.step(a)
+                                steps.append({"action": a, "obs": enc(obs),
+                                              "reward": int(r), "done": bool(done),
+                                              "turn": int(env.player_turn),
+                                              "moves": list(map(int, env.possible_moves))})
+                            games.append(steps)
+                    traces.append({"cls": cls_name, "protagonist": protagonist, "kw": kw,
+                                   "games": games})
+    with open(os.path.join(OUT, "wrappers.json"), "w") as f:
+        json.dump(traces, f, separators=(",", ":"))
+
+
+def main():
+    install_shims()
+    import othello  # noqa: E402  (reference, read-only)
+    import simple_policies  # noqa: E402
+    import util  # noqa: E402
+    gen_kat(othello)
+    gen_trajectories(othello)
+    gen_greedy(othello, simple_policies, util)
+    gen_obs(othello, util)
+    gen_wrappers(othello, simple_policies)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,150 @@
+"""Pin the CPU oracle (oracle/othello_oracle.c) to the reference's own outputs.
+
+The fixtures in tests/golden/ were produced by tests/golden/gen_golden.py, which
+imports the reference othello.py / simple_policies.py / util.py.  Every
+GPU parity test later compares the HIP path against this oracle, so this file
+is what makes those comparisons mean "identical to the reference".
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+SIZES = list(range(4, 17))
+
+
+def load_traj(golden_dir, n):
+    return dict(np.load(os.path.join(golden_dir, "traj_N%d.npz" % n)))
+
+
+def decode_meta(meta):
+    turn = np.where(meta & 1, 1, -1)
+    term = (meta >> 1) & 1
+    wc = (meta >> 2) & 3
+    winner = np.where(wc == 1, 1, np.where(wc == 2, -1, 0))
+    return turn, term, winner
+
+
+def test_kat(golden_dir):
+    kat = json.load(open(os.path.join(golden_dir, "kat.json")))
+    for n in SIZES:
+        k = kat[str(n)]
+        s = oracle.reset(n, 1)
+        W = oracle.nwords(n)
+        assert list(s.boards[0, :W]) == k["black"]
+        assert list(s.boards[0, W:]) == k["white"]
+        moves = [a for a in range(n * n) if (int(s.legal[0, a // 64]) >> (a % 64)) & 1]
+        assert moves == k["black_moves"]
+        oracle.step(s, oracle.F_SUDDEN_DEATH, np.array([moves[0]]))
+        moves2 = [a for a in range(n * n) if (int(s.legal[0, a // 64]) >> (a % 64)) & 1]
+        assert moves2 == k["white_moves_after_lowest"]
+        assert k["action_space_n"] == n * n
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_step_matches_reference_per_ply(golden_dir, n):
+    """Each recorded ply, stepped from its recorded pre-state, reproduces the
+    reference's post-state, possible_moves (incl. stale terminals), reward, done."""
+    t = load_traj(golden_dir, n)
+    combos = t["combos"]
+    for ci, (sd, dr) in enumerate(combos):
+        sel = t["combo"] == ci
+        E = int(sel.sum())
+        s = oracle.State(n, E)
+        s.boards[:] = np.concatenate([t["prev_black"][sel], t["prev_white"][sel]], axis=1)
+        s.meta[:] = oracle.meta_from(t["prev_turn"][sel])
+        s.legal[:] = t["prev_legal"][sel]
+        flags = (oracle.F_SUDDEN_DEATH if sd else 0) | (oracle.F_DISK_REWARD if dr else 0)
+        rew, dones, errs = oracle.step(s, flags, t["action"][sel])
+        assert errs == 0
+        np.testing.assert_array_equal(s.boards, np.concatenate([t["black"][sel], t["white"][sel]], axis=1))
+        np.testing.assert_array_equal(s.legal, t["legal"][sel])
+        turn, term, winner = decode_meta(s.meta)
+        np.testing.assert_array_equal(turn, t["turn"][sel])
+        np.testing.assert_array_equal(term, t["done"][sel].astype(int))
+        np.testing.assert_array_equal(winner, t["winner"][sel])
+        np.testing.assert_array_equal(rew, t["reward"][sel])
+        np.testing.assert_array_equal(dones, t["done"][sel])
+
+
+@pytest.mark.parametrize("n", [4, 5, 8, 10, 16])
+def test_whole_games_replay(golden_dir, n):
+    """Replaying each game's action list from reset reproduces every ply."""
+    t = load_traj(golden_dir, n)
+    for ci, (sd, dr) in enumerate(t["combos"]):
+        flags = (oracle.F_SUDDEN_DEATH if sd else 0) | (oracle.F_DISK_REWARD if dr else 0)
+        games = np.unique(t["game"][t["combo"] == ci])
+        for g in games:
+            sel = np.flatnonzero((t["combo"] == ci) & (t["game"] == g))
+            s = oracle.reset(n, 1)
+            for i in sel:
+                r, d, errs = oracle.step(s, flags, t["action"][i:i + 1])
+                assert errs == 0
+                assert r[0] == t["reward"][i] and d[0] == t["done"][i]
+                assert list(s.boards[0]) == list(t["black"][i]) + list(t["white"][i])
+                assert list(s.legal[0]) == list(t["legal"][i])
+            # stepping again after the terminal ply is the reference's ValueError
+            r, d, errs = oracle.step(s, flags, np.array([0]))
+            assert errs == 1 and d[0] == 1 and r[0] == 0
+
+
+def test_edge_cases_are_covered(golden_dir):
+    """The fixtures exercise every terminal / pass path the reference has."""
+    seen = {"double_pass": 0, "wipeout": 0, "sudden": 0, "invalid_pass": 0, "pass": 0}
+    for n in SIZES:
+        t = load_traj(golden_dir, n)
+        nn = n * n
+        for i in range(len(t["action"])):
+            sd, dr = t["combos"][t["combo"][i]]
+            a = int(t["action"][i])
+            invalid = not ((int(t["prev_legal"][i][a // 64]) >> (a % 64)) & 1) if 0 <= a < nn else True
+            if t["done"][i] and invalid and sd:
+                seen["sudden"] += 1
+            if invalid and not sd and not t["done"][i]:
+                seen["invalid_pass"] += 1
+            if not t["done"][i] and t["turn"][i] == t["prev_turn"][i]:
+                seen["pass"] += 1
+            full = sum(bin(int(x)).count("1") for x in (t["black"][i] | t["white"][i])) == nn
+            if t["done"][i] and not invalid and not full:
+                seen["double_pass"] += 1
+            if t["done"][i] and dr and t["reward"][i] == nn:
+                seen["wipeout"] += 1
+    for k, v in seen.items():
+        assert v > 0, k
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_greedy_matches_reference(golden_dir, n):
+    g = np.load(os.path.join(golden_dir, "greedy.npz"))
+    b, w, t, a = g["N%d_black" % n], g["N%d_white" % n], g["N%d_turn" % n], g["N%d_action" % n]
+    s = oracle.State(n, len(a))
+    s.boards[:] = np.concatenate([b, w], axis=1)
+    s.meta[:] = oracle.meta_from(t)
+    s.legal[:] = oracle.recompute_legal(s)
+    np.testing.assert_array_equal(oracle.greedy(s), a)
+
+
+@pytest.mark.parametrize("n", [6, 8])
+def test_observations_match_reference(golden_dir, n):
+    o = np.load(os.path.join(golden_dir, "obs.npz"))
+    s = oracle.State(n, len(o["N%d_turn" % n]))
+    s.boards[:] = np.concatenate([o["N%d_black" % n], o["N%d_white" % n]], axis=1)
+    s.meta[:] = oracle.meta_from(o["N%d_turn" % n])
+    s.legal[:] = o["N%d_legal" % n]
+    obs, obs2, ms = oracle.observe(s)
+    np.testing.assert_array_equal(obs, o["N%d_obs" % n])
+    np.testing.assert_array_equal(obs2, o["N%d_obs2" % n])
+    np.testing.assert_array_equal(ms, o["N%d_make_state" % n].astype(np.float32))
+    assert (o["N%d_nlegal" % n] == 1).any()  # the single-legal-move quirk is exercised
+
+
+def test_random_policy_distribution():
+    """Philox random play: outcome split near the reference's (46/4/49 %)."""
+    s = oracle.reset(8, 2000)
+    _, _, dones, wdl = oracle.rollout(s, oracle.F_SUDDEN_DEATH, 0, 64, seed=0)
+    assert wdl.sum() == 2000  # every 8x8 random game ends within 60 + passes <= 64 plies
+    frac = wdl / wdl.sum()
+    assert 0.40 < frac[0] < 0.52 and 0.02 < frac[1] < 0.08 and 0.43 < frac[2] < 0.56
