@@ -1,0 +1,194 @@
+#!/usr/bin/env python3
+"""Benchmark: env-steps/s of on-device random play on 65,536 8x8 boards per GPU
+(BASELINE.json `metric`, config 2; N GPUs = config 4's weak-scaled shards).
+
+A step = one ply applied to every board of the shard (one OthelloBaseEnv.step
+per board, pass resolution included), the mover choosing uniformly among its
+possible_moves (RandomPolicy, simple_policies.py:37-41) from a Philox stream;
+finished games auto-reset.  Boards, actions, rewards and dones stay in HBM.
+`--plies-per-launch P` runs P plies per kernel launch (board state kept in
+registers between plies, every ply's action / reward / done still stored).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU, RCCL)
+
+Rank 0 prints one JSON line.  `roofline` prices the dominant kernel
+(k_play<8, random>) by its algorithmic HBM bytes per launch over its average
+launch time (HIP events on the launch stream); `traffic` comes from the
+rocprofv3 PMC summary committed under profiles/ (null if absent).
+`cpu_baseline` times the oracle's scalar restatement of othello.py on a host
+core over a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def algorithmic_bytes_per_launch(E, W, plies, record=True):
+    """HBM bytes one k_play launch must move: board state in and out once
+    (boards 16W + legal 8W + meta 2, each way) plus per ply the action (4),
+    reward (4) and done (1) of every board."""
+    state = 2 * (16 * W + 8 * W + 2)
+    per_ply = (4 + 4 + 1) if record else 0
+    return E * (state + plies * per_ply)
+
+
+def cpu_baseline(seconds, board_size=8):
+    """Scalar restatement of the reference rules engine (oracle/, the per-cell
+    8-direction ray walk of othello.py:273-343) with the same random policy and
+    auto-reset, single-threaded; bounded sample of ~`seconds` of CPU work."""
+    from oracle import oracle
+    E, chunk = 1024, 16
+    s = oracle.reset(board_size, E)
+    flags = oracle.F_SUDDEN_DEATH | oracle.F_AUTO_RESET
+    plies = 0
+    t0 = time.perf_counter()
+    while True:
+        oracle.rollout(s, flags, 0, chunk, seed=0, ply0=plies, record=False)
+        plies += chunk
+        dt = time.perf_counter() - t0
+        if dt >= seconds:
+            break
+    steps = E * plies
+    return {"value": steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": "%d boards x %d plies (%d env-steps) of random play, %dx%d, auto-reset, "
+                      "oracle/othello_oracle.c scalar ray-scan restatement of othello.py, 1 thread, %.1f s"
+                      % (E, plies, steps, board_size, board_size, dt)}
+
+
+def load_traffic(workload):
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+        rec = d.get(workload)
+        return None if rec is None else rec["hbm_bytes_per_launch"]
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--envs", type=int, default=65536, help="boards per GPU")
+    ap.add_argument("--board-size", type=int, default=8)
+    ap.add_argument("--policy", default="random", choices=["random", "greedy"])
+    ap.add_argument("--plies-per-launch", type=int, default=None)
+    ap.add_argument("--no-record", action="store_true", help="do not store per-ply action/reward/done")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from gymothelloenv_amd import VecOthelloEnv
+    from gymothelloenv_amd.vec_env import nwords
+
+    E, n = args.envs, args.board_size
+    W = nwords(n)
+    P = args.plies_per_launch or (50 if args.policy == "random" else 10)
+    steps = max(P, (args.steps // P) * P)
+    warm = max(P, (args.warmup // P) * P) if args.warmup > 0 else 0
+    launches = steps // P
+    record = not args.no_record
+    env = VecOthelloEnv(E, board_size=n, auto_reset=True, seed=0, env_id_base=rank * E,
+                        initial_rand_steps=10 if args.policy == "greedy" else 0, device=dev)
+    env.reset()
+    acts = torch.empty(P, E, dtype=torch.int32, device=dev) if record else None
+    rews = torch.empty(P, E, dtype=torch.int32, device=dev) if record else None
+    dns = torch.empty(P, E, dtype=torch.uint8, device=dev) if record else None
+
+    def run(k_launches):
+        for _ in range(k_launches):
+            env.step_policy(args.policy, n_plies=P, actions=acts, rewards=rews, dones=dns, record=record)
+
+    run(warm // P)
+    env.counts(reset=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    run(launches)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1)  # HIP events on the launch stream
+    wdl = env.counts()
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        gathered = torch.empty(world * 3, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(gathered, wdl)  # RCCL over xGMI: the W/D/L tally
+        wdl_total = gathered.view(world, 3).sum(0)
+    else:
+        wdl_total = wdl
+    wall_max = float(t.item())
+    wdl_total = [int(x) for x in wdl_total.cpu().tolist()]
+
+    if rank == 0:
+        total_steps = E * world * steps
+        value = total_steps / wall_max
+        avg_launch_s = kern_ms / 1e3 / launches
+        bytes_launch = algorithmic_bytes_per_launch(E, W, P, record)
+        achieved = bytes_launch / avg_launch_s / 1e9
+        workload = "random-play-%dx%d-E%d-P%d" % (n, n, E, P) if args.policy == "random" else \
+            "greedy-play-%dx%d-E%d-P%d" % (n, n, E, P)
+        out = {
+            "metric": "env-steps/sec (random policy, 65,536x8x8 boards per GPU)" if args.policy == "random"
+            else "env-steps/sec (greedy policy)",
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": steps,
+            "warmup": warm,
+            "ms_per_step": wall_max / steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (standard opening, Philox random play, auto-reset)",
+            "config": {"workload": workload, "boards_per_gpu": E, "board_size": n,
+                       "global_boards": E * world, "plies_per_launch": P, "policy": args.policy,
+                       "per_ply_outputs_stored": record, "parallelism": "dp%d (independent shards)" % world},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBPS, "traffic": load_traffic(workload),
+                         "kernel": "k_play<%d,%s>" % (n, args.policy), "avg_launch_us": avg_launch_s * 1e6,
+                         "algorithmic_bytes_per_launch": bytes_launch},
+            "wdl": {"black_wins": wdl_total[0], "draws": wdl_total[1], "white_wins": wdl_total[2]},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, n)
+        print(json.dumps(out), flush=True)
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

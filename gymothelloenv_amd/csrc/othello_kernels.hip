@@ -1,0 +1,765 @@
+// othello_kernels.hip -- HIP/CDNA4 kernels of the vectorised Othello rules
+// engine and the C ABI declared in include/othello_mi355x.h.
+//
+// One board per lane.  A board is two W-word bitboards (black, white) held in
+// VGPRs; legal moves and flips are Kogge-Stone occluded fills (bitboard.hpp).
+// The reference's per-step Python work -- get_possible_actions'
+// N*N*8 ray walks (othello.py:313-343), update_board (:391-410), step's
+// pass / double-pass / sudden-death / reward logic (:412-462) -- becomes a few
+// hundred integer VALU ops per lane.  No MFMA: the work is bit manipulation.
+//
+// HBM layout (exchange format, see the header): boards [E][2W] u64 (a lane
+// reads 16W contiguous bytes: dwordx4 loads), meta [E] u16, legal [E][W] u64;
+// per-ply outputs are [ply][E] so every store instruction is coalesced.
+#include <hip/hip_runtime.h>
+
+#include <stdio.h>
+#include <string.h>
+
+#include <new>
+#include <string>
+#include <type_traits>
+
+#include "bitboard.hpp"
+#include "othello_mi355x.h"
+
+using namespace oth;
+
+namespace {
+
+constexpr int BLOCK = 256;
+constexpr uint32_t M_TURN_WHITE = 1u;
+constexpr uint32_t M_TERMINATED = 2u;
+constexpr int M_WINNER_SHIFT = 2;
+constexpr int M_RAND_SHIFT = 8;
+constexpr int BLACK_DISK = -1, NO_DISK = 0, WHITE_DISK = 1;  // othello.py:10-12
+
+// Philox "purpose" word: which decision a draw feeds.
+constexpr uint32_t RNG_ACTION = 0, RNG_OPENING_AUTO = 1, RNG_OPENING_RESET = 2;
+
+template <int N>
+struct Start {  // _reset_board (othello.py:256-263): W at (c-1,c-1),(c,c); B at (c,c-1),(c-1,c)
+    static constexpr int W = Geo<N>::W;
+    static constexpr int C = N / 2;
+    static constexpr BB<W> make(int a0, int a1) {
+        BB<W> b{};
+        for (int i = 0; i < W; ++i) b.w[i] = 0;
+        b.w[a0 / 64] |= 1ull << (a0 % 64);
+        b.w[a1 / 64] |= 1ull << (a1 % 64);
+        return b;
+    }
+    static constexpr BB<W> BLACK = make(C * N + (C - 1), (C - 1) * N + C);
+    static constexpr BB<W> WHITE = make((C - 1) * N + (C - 1), C * N + C);
+};
+
+template <int N>
+struct Lane {
+    static constexpr int W = Geo<N>::W;
+    BB<W> black, white, legal;
+    uint32_t meta;
+};
+
+template <int N>
+__device__ __forceinline__ void load_lane(Lane<N>& s, const uint64_t* __restrict__ boards,
+                                          const uint16_t* __restrict__ meta, const uint64_t* __restrict__ legal,
+                                          int e) {
+    constexpr int W = Geo<N>::W;
+    const ulonglong2* bp = reinterpret_cast<const ulonglong2*>(boards) + (size_t)e * W;
+    uint64_t tmp[2 * W];
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+        ulonglong2 v = bp[i];
+        tmp[2 * i] = v.x;
+        tmp[2 * i + 1] = v.y;
+    }
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+        s.black.w[i] = tmp[i];
+        s.white.w[i] = tmp[W + i];
+        s.legal.w[i] = legal[(size_t)e * W + i];
+    }
+    s.meta = meta[e];
+}
+
+template <int N>
+__device__ __forceinline__ void store_lane(const Lane<N>& s, uint64_t* __restrict__ boards,
+                                           uint16_t* __restrict__ meta, uint64_t* __restrict__ legal, int e) {
+    constexpr int W = Geo<N>::W;
+    uint64_t tmp[2 * W];
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+        tmp[i] = s.black.w[i];
+        tmp[W + i] = s.white.w[i];
+    }
+    ulonglong2* bp = reinterpret_cast<ulonglong2*>(boards) + (size_t)e * W;
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+        ulonglong2 v;
+        v.x = tmp[2 * i];
+        v.y = tmp[2 * i + 1];
+        bp[i] = v;
+        legal[(size_t)e * W + i] = s.legal.w[i];
+    }
+    meta[e] = (uint16_t)s.meta;
+}
+
+// OthelloBaseEnv.reset (othello.py:265-271); rand_left = SimpleOthelloEnv's
+// random-opening length randint(0, k//2+1)*2 (othello.py:62-63) from Philox.
+template <int N>
+__device__ __forceinline__ void reset_lane(Lane<N>& s, uint64_t seed, uint32_t id, uint64_t ply, uint32_t purpose,
+                                           int init_rand) {
+    s.black = Start<N>::BLACK;
+    s.white = Start<N>::WHITE;
+    s.legal = legal_moves<N>(s.black, s.white);  // black moves first (othello.py:267)
+    uint32_t rl = 0;
+    if (init_rand > 0) rl = (uint32_t)scale_index(philox_x(seed, id, ply, purpose), init_rand / 2 + 1) * 2u;
+    s.meta = (rl & 0xffu) << M_RAND_SHIFT;
+}
+
+// OthelloBaseEnv.step (othello.py:412-462) for one lane.  Returns the winner
+// code (0 none) through `winner` when the game ends on this ply.
+template <int N>
+__device__ __forceinline__ void step_lane(Lane<N>& s, int a, uint32_t flags, int& reward, int& done, int& winner) {
+    constexpr int W = Geo<N>::W;
+    constexpr int NN = N * N;
+    winner = NO_DISK;
+    if (s.meta & M_TERMINATED) {  // reference: ValueError (othello.py:415-416)
+        reward = 0;
+        done = 1;
+        return;
+    }
+    const bool tw = (s.meta & M_TURN_WHITE) != 0;
+    BB<W> P = tw ? s.white : s.black;
+    BB<W> O = tw ? s.black : s.white;
+    const bool valid = a >= 0 && a < NN && test(s.legal, a);  // `action not in possible_moves` (:417)
+    if (valid) {                                               // update_board (:391-410)
+        const BB<W> m = square<W>(a);
+        const BB<W> f = flips<N>(P, O, m);
+        P |= f | m;
+        O = O & ~(f | m);
+    }
+    const bool full = !any(~(P | O) & Geo<N>::BOARD);                       // :425-426
+    const bool sudden = !valid && (flags & OTH_SUDDEN_DEATH);              // :427
+    const int pc = popcount(P), oc = popcount(O);
+    const int cur = tw ? WHITE_DISK : BLACK_DISK;
+    const int by_count = pc > oc ? cur : (pc < oc ? -cur : NO_DISK);       // determine_winner (:486-501)
+    bool term = false, new_tw = tw;
+    if (sudden || full) {  // :431-433 -- turn and possible_moves stay stale
+        term = true;
+        winner = sudden ? -cur : by_count;  // :475-485
+    } else {               // :436-442
+        const BB<W> om = legal_moves<N>(O, P);
+        if (any(om)) {
+            new_tw = !tw;
+            s.legal = om;
+        } else {  // opponent passes; mover again, or nobody can move
+            const BB<W> mm = legal_moves<N>(P, O);
+            s.legal = mm;
+            if (!any(mm)) {
+                term = true;
+                winner = by_count;
+            }
+        }
+    }
+    if (tw) {
+        s.white = P;
+        s.black = O;
+    } else {
+        s.black = P;
+        s.white = O;
+    }
+    int r = 0;  // :444-461
+    if (term) {
+        if (flags & OTH_DISK_REWARD) {
+            r = sudden ? -NN : (oc == 0 ? NN : pc - oc);
+        } else {
+            r = winner * cur;
+        }
+    }
+    const uint32_t wcode = winner == WHITE_DISK ? 1u : (winner == BLACK_DISK ? 2u : 0u);
+    s.meta = (s.meta & 0xff00u) | (new_tw ? M_TURN_WHITE : 0u) | (term ? M_TERMINATED : 0u) |
+             (term ? (wcode << M_WINNER_SHIFT) : 0u);
+    reward = r;
+    done = term ? 1 : 0;
+}
+
+// RandomPolicy.get_action (simple_policies.py:37-41): possible_moves[randint(len)].
+template <int N>
+__device__ __forceinline__ int random_action(const Lane<N>& s, uint64_t seed, uint32_t id, uint64_t ply) {
+    const int n = popcount(s.legal);
+    const int k = scale_index(philox_x(seed, id, ply, RNG_ACTION), n);
+    return select_bit(s.legal, k);
+}
+
+// GreedyPolicy.get_action (simple_policies.py:69-92): the move that leaves the
+// mover the most discs = the most flips; np.argmax keeps the first (lowest
+// square) of equal counts, so scan ascending and replace only on '>'.
+template <int N>
+__device__ __forceinline__ int greedy_action(const Lane<N>& s) {
+    constexpr int W = Geo<N>::W;
+    const bool tw = (s.meta & M_TURN_WHITE) != 0;
+    const BB<W> P = tw ? s.white : s.black;
+    const BB<W> O = tw ? s.black : s.white;
+    int best = -1, best_cnt = -1;
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+        uint64_t x = s.legal.w[i];
+        while (x) {
+            const int b = __builtin_ctzll(x);
+            x &= x - 1;
+            BB<W> m = zero<W>();
+            m.w[i] = 1ull << b;
+            const int c = popcount(flips<N>(P, O, m));
+            if (c > best_cnt) {
+                best_cnt = c;
+                best = 64 * i + b;
+            }
+        }
+    }
+    return best;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ void tally(unsigned long long* wdl, uint32_t b, uint32_t d, uint32_t w) {
+    b = wave_sum(b);
+    d = wave_sum(d);
+    w = wave_sum(w);
+    if ((threadIdx.x & 63) == 0 && wdl) {
+        if (b) atomicAdd(wdl + 0, (unsigned long long)b);
+        if (d) atomicAdd(wdl + 1, (unsigned long long)d);
+        if (w) atomicAdd(wdl + 2, (unsigned long long)w);
+    }
+}
+
+struct Rng {
+    uint64_t seed;
+    uint32_t id_base;
+    int init_rand;
+};
+
+template <int N>
+__global__ __launch_bounds__(BLOCK) void k_reset(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
+                                                 uint64_t* __restrict__ legal, int E,
+                                                 const uint8_t* __restrict__ mask, Rng rng, uint64_t ply) {
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= E) return;
+    if (mask && !mask[e]) return;
+    Lane<N> s;
+    reset_lane<N>(s, rng.seed, rng.id_base + (uint32_t)e, ply, RNG_OPENING_RESET, rng.init_rand);
+    store_lane<N>(s, boards, meta, legal, e);
+}
+
+// oth_step: external actions, one ply.
+template <int N>
+__global__ __launch_bounds__(BLOCK) void k_step(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
+                                                uint64_t* __restrict__ legal, int E, uint32_t flags,
+                                                const int32_t* __restrict__ actions, int32_t* __restrict__ rewards,
+                                                uint8_t* __restrict__ dones, unsigned long long* __restrict__ wdl,
+                                                Rng rng, uint64_t ply) {
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    uint32_t cb = 0, cd = 0, cw = 0;
+    if (e < E) {
+        Lane<N> s;
+        load_lane<N>(s, boards, meta, legal, e);
+        const bool was_term = (s.meta & M_TERMINATED) != 0;
+        int r, d, win;
+        step_lane<N>(s, actions[e], flags, r, d, win);
+        if (d && !was_term) {
+            cb = win == BLACK_DISK;
+            cd = win == NO_DISK;
+            cw = win == WHITE_DISK;
+            if (flags & OTH_AUTO_RESET)
+                reset_lane<N>(s, rng.seed, rng.id_base + (uint32_t)e, ply, RNG_OPENING_AUTO, rng.init_rand);
+        }
+        store_lane<N>(s, boards, meta, legal, e);
+        if (rewards) rewards[e] = r;
+        if (dones) dones[e] = (uint8_t)d;
+    }
+    tally(wdl, cb, cd, cw);
+}
+
+// oth_step_policy: `plies` plies of on-device play with the board kept in
+// registers between plies; per-ply outputs stored [ply][E].
+template <int N, int POLICY>
+__global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
+                                                uint64_t* __restrict__ legal, int E, uint32_t flags, int plies,
+                                                int32_t* __restrict__ actions, int32_t* __restrict__ rewards,
+                                                uint8_t* __restrict__ dones, unsigned long long* __restrict__ wdl,
+                                                Rng rng, uint64_t ply0) {
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    uint32_t cb = 0, cd = 0, cw = 0;
+    if (e < E) {
+        const uint32_t id = rng.id_base + (uint32_t)e;
+        Lane<N> s;
+        load_lane<N>(s, boards, meta, legal, e);
+        for (int p = 0; p < plies; ++p) {
+            const uint64_t g = ply0 + (uint64_t)p;
+            const size_t o = (size_t)p * (size_t)E + (size_t)e;
+            int a = -1, r = 0, d = 1, win = NO_DISK;
+            if (!(s.meta & M_TERMINATED)) {
+                const uint32_t rl = s.meta >> M_RAND_SHIFT;
+                if (POLICY == OTH_POLICY_RANDOM || rl > 0) {
+                    a = random_action<N>(s, rng.seed, id, g);
+                    if (rl > 0) s.meta -= 1u << M_RAND_SHIFT;
+                } else {
+                    a = greedy_action<N>(s);
+                }
+                step_lane<N>(s, a, flags, r, d, win);
+                if (d) {
+                    cb += win == BLACK_DISK;
+                    cd += win == NO_DISK;
+                    cw += win == WHITE_DISK;
+                    if (flags & OTH_AUTO_RESET)
+                        reset_lane<N>(s, rng.seed, id, g, RNG_OPENING_AUTO, rng.init_rand);
+                }
+            }
+            if (actions) actions[o] = a;
+            if (rewards) rewards[o] = r;
+            if (dones) dones[o] = (uint8_t)d;
+        }
+        store_lane<N>(s, boards, meta, legal, e);
+    }
+    tally(wdl, cb, cd, cw);
+}
+
+template <int N>
+__global__ __launch_bounds__(BLOCK) void k_legal_moves(const uint64_t* __restrict__ mover,
+                                                       const uint64_t* __restrict__ opp, uint64_t* __restrict__ out,
+                                                       int n) {
+    constexpr int W = Geo<N>::W;
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= n) return;
+    BB<W> P, O;
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+        P.w[i] = mover[(size_t)e * W + i] & Geo<N>::BOARD.w[i];
+        O.w[i] = opp[(size_t)e * W + i] & Geo<N>::BOARD.w[i] & ~P.w[i];
+    }
+    const BB<W> L = legal_moves<N>(P, O);
+#pragma unroll
+    for (int i = 0; i < W; ++i) out[(size_t)e * W + i] = L.w[i];
+}
+
+template <int N>
+__global__ __launch_bounds__(BLOCK) void k_greedy(const uint64_t* __restrict__ boards,
+                                                  const uint16_t* __restrict__ meta,
+                                                  const uint64_t* __restrict__ legal, int E,
+                                                  int32_t* __restrict__ out) {
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= E) return;
+    Lane<N> s;
+    load_lane<N>(s, boards, meta, legal, e);
+    out[e] = greedy_action<N>(s);
+}
+
+template <int N>
+__global__ __launch_bounds__(BLOCK) void k_set_turn(const uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
+                                                    uint64_t* __restrict__ legal, int E, int turn,
+                                                    const uint8_t* __restrict__ mask) {
+    constexpr int W = Geo<N>::W;
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= E) return;
+    if (mask && !mask[e]) return;
+    BB<W> b, w;
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+        b.w[i] = boards[(size_t)e * 2 * W + i];
+        w.w[i] = boards[(size_t)e * 2 * W + W + i];
+    }
+    const BB<W> L = turn == WHITE_DISK ? legal_moves<N>(w, b) : legal_moves<N>(b, w);
+#pragma unroll
+    for (int i = 0; i < W; ++i) legal[(size_t)e * W + i] = L.w[i];
+    meta[e] = (uint16_t)((meta[e] & ~M_TURN_WHITE) | (turn == WHITE_DISK ? M_TURN_WHITE : 0u));
+}
+
+template <int N>
+__global__ __launch_bounds__(BLOCK) void k_count(const uint64_t* __restrict__ boards, int E,
+                                                 int32_t* __restrict__ out) {
+    constexpr int W = Geo<N>::W;
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= E) return;
+    int b = 0, w = 0;
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+        b += popc64(boards[(size_t)e * 2 * W + i]);
+        w += popc64(boards[(size_t)e * 2 * W + W + i]);
+    }
+    out[2 * (size_t)e] = w;
+    out[2 * (size_t)e + 1] = b;
+}
+
+template <typename T>
+__device__ __forceinline__ void put(void* out, size_t i, int v) {
+    reinterpret_cast<T*>(out)[i] = (T)v;
+}
+
+// One thread per output element, (E, planes, N, N) row-major: coalesced stores.
+template <int N>
+__global__ __launch_bounds__(BLOCK) void k_observe(const uint64_t* __restrict__ boards,
+                                                   const uint16_t* __restrict__ meta,
+                                                   const uint64_t* __restrict__ legal, int E, int layout, int dtype,
+                                                   void* __restrict__ out) {
+    constexpr int W = Geo<N>::W;
+    constexpr int NN = N * N;
+    const int planes = layout == OTH_OBS_BOARD_LEGAL ? 2 : (layout == OTH_OBS_MAKE_STATE ? 4 : 1);
+    const size_t total = (size_t)E * planes * NN;
+    for (size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x; i < total; i += (size_t)gridDim.x * BLOCK) {
+        const int a = (int)(i % NN);
+        const size_t rest = i / NN;
+        const int plane = (int)(rest % planes);
+        const size_t e = rest / planes;
+        const int wi = a / 64, bi = a % 64;
+        const int isb = (int)((boards[e * 2 * W + wi] >> bi) & 1u);
+        const int isw = (int)((boards[e * 2 * W + W + wi] >> bi) & 1u);
+        const uint32_t m = meta[e];
+        const bool tw = (m & M_TURN_WHITE) != 0;
+        int v;
+        if (layout == OTH_OBS_ABSOLUTE) {
+            v = isw - isb;
+        } else if (layout == OTH_OBS_MAKE_STATE) {
+            if (plane == 0) {
+                v = isb;
+            } else if (plane == 1) {
+                v = isw;
+            } else if (plane == 2) {
+                v = tw ? 1 : 0;
+            } else {  // util.py:55: the legal plane only when >= 2 moves
+                int cnt = 0;
+#pragma unroll
+                for (int k = 0; k < W; ++k) cnt += popc64(legal[e * W + k]);
+                v = cnt > 1 ? (int)((legal[e * W + wi] >> bi) & 1u) : 0;
+            }
+        } else {
+            if (plane == 0) {
+                v = tw ? (isw - isb) : (isb - isw);  // othello.py:364-369
+            } else {
+                v = (int)((legal[e * W + wi] >> bi) & 1u);
+            }
+        }
+        switch (dtype) {
+            case OTH_I8: put<int8_t>(out, i, v); break;
+            case OTH_I32: put<int32_t>(out, i, v); break;
+            case OTH_I64: put<int64_t>(out, i, v); break;
+            case OTH_F32: put<float>(out, i, v); break;
+            default: put<double>(out, i, v); break;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------
+thread_local std::string g_last_error;
+
+int fail(int code, const char* msg) {
+    g_last_error = msg;
+    return code;
+}
+
+int hip_fail(hipError_t err, const char* where) {
+    char buf[256];
+    snprintf(buf, sizeof(buf), "%s: %s", where, hipGetErrorString(err));
+    g_last_error = buf;
+    return OTH_EHIP;
+}
+
+#define OTH_HIP(call)                                       \
+    do {                                                    \
+        hipError_t err_ = (call);                           \
+        if (err_ != hipSuccess) return hip_fail(err_, #call); \
+    } while (0)
+
+int after_launch(const char* what) {
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return hip_fail(err, what);
+    return OTH_OK;
+}
+
+template <typename Fn>
+int with_n(int n, Fn&& fn) {
+    switch (n) {
+        case 4: return fn(std::integral_constant<int, 4>{});
+        case 5: return fn(std::integral_constant<int, 5>{});
+        case 6: return fn(std::integral_constant<int, 6>{});
+        case 7: return fn(std::integral_constant<int, 7>{});
+        case 8: return fn(std::integral_constant<int, 8>{});
+        case 9: return fn(std::integral_constant<int, 9>{});
+        case 10: return fn(std::integral_constant<int, 10>{});
+        case 11: return fn(std::integral_constant<int, 11>{});
+        case 12: return fn(std::integral_constant<int, 12>{});
+        case 13: return fn(std::integral_constant<int, 13>{});
+        case 14: return fn(std::integral_constant<int, 14>{});
+        case 15: return fn(std::integral_constant<int, 15>{});
+        case 16: return fn(std::integral_constant<int, 16>{});
+        default: return fail(OTH_EINVAL, "board_size must be in [4, 16]");
+    }
+}
+
+int grid_for(long long work) { return (int)((work + BLOCK - 1) / BLOCK); }
+
+}  // namespace
+
+struct oth_env {
+    int32_t E;
+    int32_t n;
+    int32_t W;
+    uint32_t flags;
+    uint64_t seed;
+    uint32_t id_base;
+    int32_t init_rand;
+    int32_t device;
+    uint64_t ply;
+    uint64_t* boards;
+    uint16_t* meta;
+    uint64_t* legal;
+    unsigned long long* wdl;
+};
+
+namespace {
+int use_device(const oth_env* env) {
+    int cur = -1;
+    OTH_HIP(hipGetDevice(&cur));
+    if (cur != env->device) OTH_HIP(hipSetDevice(env->device));
+    return OTH_OK;
+}
+
+#define OTH_CHECK_ENV(env)                                                  \
+    do {                                                                    \
+        if (!(env)) return fail(OTH_EINVAL, "NULL oth_env");               \
+        int rc_ = use_device(env);                                          \
+        if (rc_) return rc_;                                                \
+    } while (0)
+
+Rng rng_of(const oth_env* env) { return Rng{env->seed, env->id_base, env->init_rand}; }
+}  // namespace
+
+extern "C" {
+
+const char* oth_last_error(void) { return g_last_error.c_str(); }
+
+const char* oth_version(void) { return "othello_mi355x 0.1 (gfx950)"; }
+
+int oth_create(int32_t n_envs, int32_t board_size, uint32_t flags, uint64_t seed, uint32_t env_id_base,
+               int32_t initial_rand_steps, int32_t device, oth_env** out) {
+    if (!out) return fail(OTH_EINVAL, "out is NULL");
+    *out = nullptr;
+    if (n_envs <= 0) return fail(OTH_EINVAL, "n_envs must be > 0");
+    const int n = board_size < 4 ? 4 : board_size;  // othello.py:230
+    if (n > 16) return fail(OTH_EINVAL, "board_size must be <= 16");
+    if (initial_rand_steps < 0 || initial_rand_steps > 255)
+        return fail(OTH_EINVAL, "initial_rand_steps must be in [0, 255]");
+    if (flags & ~7u) return fail(OTH_EINVAL, "unknown flag bits");
+    OTH_HIP(hipSetDevice(device));
+    oth_env* env = new (std::nothrow) oth_env();
+    if (!env) return fail(OTH_ENOMEM, "host allocation failed");
+    env->E = n_envs;
+    env->n = n;
+    env->W = (n * n + 63) / 64;
+    env->flags = flags;
+    env->seed = seed;
+    env->id_base = env_id_base;
+    env->init_rand = initial_rand_steps;
+    env->device = device;
+    env->ply = 0;
+    const size_t E = (size_t)n_envs, W = (size_t)env->W;
+    hipError_t err = hipMalloc((void**)&env->boards, E * 2 * W * sizeof(uint64_t));
+    if (err == hipSuccess) err = hipMalloc((void**)&env->meta, ((E * sizeof(uint16_t) + 15) / 16) * 16);
+    if (err == hipSuccess) err = hipMalloc((void**)&env->legal, E * W * sizeof(uint64_t));
+    if (err == hipSuccess) err = hipMalloc((void**)&env->wdl, 4 * sizeof(unsigned long long));
+    if (err == hipSuccess) err = hipMemset(env->wdl, 0, 4 * sizeof(unsigned long long));
+    if (err != hipSuccess) {
+        oth_destroy(env);
+        return hip_fail(err, "oth_create: allocation");
+    }
+    int rc = oth_reset(env, nullptr, nullptr);
+    if (rc == OTH_OK) {
+        err = hipStreamSynchronize(nullptr);
+        if (err != hipSuccess) rc = hip_fail(err, "oth_create: reset");
+    }
+    if (rc != OTH_OK) {
+        oth_destroy(env);
+        return rc;
+    }
+    *out = env;
+    return OTH_OK;
+}
+
+int oth_destroy(oth_env* env) {
+    if (!env) return OTH_OK;
+    (void)hipSetDevice(env->device);
+    if (env->boards) (void)hipFree(env->boards);
+    if (env->meta) (void)hipFree(env->meta);
+    if (env->legal) (void)hipFree(env->legal);
+    if (env->wdl) (void)hipFree(env->wdl);
+    delete env;
+    return OTH_OK;
+}
+
+int oth_reset(oth_env* env, const uint8_t* mask, oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    return with_n(env->n, [&](auto NC) {
+        constexpr int N = decltype(NC)::value;
+        hipLaunchKernelGGL(k_reset<N>, dim3(grid_for(env->E)), dim3(BLOCK), 0, (hipStream_t)stream, env->boards,
+                           env->meta, env->legal, env->E, mask, rng_of(env), env->ply);
+        return after_launch("oth_reset");
+    });
+}
+
+int oth_step(oth_env* env, const int32_t* actions, int32_t* rewards, uint8_t* dones, oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    if (!actions) return fail(OTH_EINVAL, "actions is NULL");
+    const uint64_t ply = env->ply++;
+    return with_n(env->n, [&](auto NC) {
+        constexpr int N = decltype(NC)::value;
+        hipLaunchKernelGGL(k_step<N>, dim3(grid_for(env->E)), dim3(BLOCK), 0, (hipStream_t)stream, env->boards,
+                           env->meta, env->legal, env->E, env->flags, actions, rewards, dones, env->wdl,
+                           rng_of(env), ply);
+        return after_launch("oth_step");
+    });
+}
+
+int oth_step_policy(oth_env* env, int32_t policy, int32_t n_plies, int32_t* actions, int32_t* rewards,
+                    uint8_t* dones, oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    if (n_plies < 0) return fail(OTH_EINVAL, "n_plies must be >= 0");
+    if (policy != OTH_POLICY_RANDOM && policy != OTH_POLICY_GREEDY) return fail(OTH_EINVAL, "unknown policy");
+    if (n_plies == 0) return OTH_OK;
+    const uint64_t ply0 = env->ply;
+    env->ply += (uint64_t)n_plies;
+    return with_n(env->n, [&](auto NC) {
+        constexpr int N = decltype(NC)::value;
+        if (policy == OTH_POLICY_RANDOM)
+            hipLaunchKernelGGL((k_play<N, OTH_POLICY_RANDOM>), dim3(grid_for(env->E)), dim3(BLOCK), 0,
+                               (hipStream_t)stream, env->boards, env->meta, env->legal, env->E, env->flags, n_plies,
+                               actions, rewards, dones, env->wdl, rng_of(env), ply0);
+        else
+            hipLaunchKernelGGL((k_play<N, OTH_POLICY_GREEDY>), dim3(grid_for(env->E)), dim3(BLOCK), 0,
+                               (hipStream_t)stream, env->boards, env->meta, env->legal, env->E, env->flags, n_plies,
+                               actions, rewards, dones, env->wdl, rng_of(env), ply0);
+        return after_launch("oth_step_policy");
+    });
+}
+
+int oth_legal(oth_env* env, uint64_t* out, oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    if (!out) return fail(OTH_EINVAL, "out is NULL");
+    OTH_HIP(hipMemcpyAsync(out, env->legal, (size_t)env->E * env->W * sizeof(uint64_t), hipMemcpyDeviceToDevice,
+                           (hipStream_t)stream));
+    return OTH_OK;
+}
+
+int oth_legal_moves(int32_t board_size, int32_t n, const uint64_t* mover, const uint64_t* opp, uint64_t* out,
+                    oth_stream_t stream) {
+    if (n < 0 || (n > 0 && (!mover || !opp || !out))) return fail(OTH_EINVAL, "bad arguments");
+    if (n == 0) return OTH_OK;
+    const int bs = board_size < 4 ? 4 : board_size;
+    return with_n(bs, [&](auto NC) {
+        constexpr int N = decltype(NC)::value;
+        hipLaunchKernelGGL(k_legal_moves<N>, dim3(grid_for(n)), dim3(BLOCK), 0, (hipStream_t)stream, mover, opp,
+                           out, n);
+        return after_launch("oth_legal_moves");
+    });
+}
+
+int oth_greedy_actions(oth_env* env, int32_t* out, oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    if (!out) return fail(OTH_EINVAL, "out is NULL");
+    return with_n(env->n, [&](auto NC) {
+        constexpr int N = decltype(NC)::value;
+        hipLaunchKernelGGL(k_greedy<N>, dim3(grid_for(env->E)), dim3(BLOCK), 0, (hipStream_t)stream, env->boards,
+                           env->meta, env->legal, env->E, out);
+        return after_launch("oth_greedy_actions");
+    });
+}
+
+int oth_observe(oth_env* env, int32_t layout, int32_t dtype, void* out, oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    if (!out) return fail(OTH_EINVAL, "out is NULL");
+    if (layout < OTH_OBS_BOARD || layout > OTH_OBS_ABSOLUTE) return fail(OTH_EINVAL, "unknown layout");
+    if (dtype < OTH_I8 || dtype > OTH_F64) return fail(OTH_EINVAL, "unknown dtype");
+    const int planes = layout == OTH_OBS_BOARD_LEGAL ? 2 : (layout == OTH_OBS_MAKE_STATE ? 4 : 1);
+    const long long total = (long long)env->E * planes * env->n * env->n;
+    int grid = grid_for(total);
+    if (grid > 65536) grid = 65536;
+    return with_n(env->n, [&](auto NC) {
+        constexpr int N = decltype(NC)::value;
+        hipLaunchKernelGGL(k_observe<N>, dim3(grid), dim3(BLOCK), 0, (hipStream_t)stream, env->boards, env->meta,
+                           env->legal, env->E, layout, dtype, out);
+        return after_launch("oth_observe");
+    });
+}
+
+int oth_get_state(oth_env* env, uint64_t* boards, uint16_t* meta, uint64_t* legal, oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    const size_t E = (size_t)env->E, W = (size_t)env->W;
+    hipStream_t s = (hipStream_t)stream;
+    if (boards) OTH_HIP(hipMemcpyAsync(boards, env->boards, E * 2 * W * 8, hipMemcpyDefault, s));
+    if (meta) OTH_HIP(hipMemcpyAsync(meta, env->meta, E * 2, hipMemcpyDefault, s));
+    if (legal) OTH_HIP(hipMemcpyAsync(legal, env->legal, E * W * 8, hipMemcpyDefault, s));
+    return OTH_OK;
+}
+
+int oth_set_state(oth_env* env, const uint64_t* boards, const uint16_t* meta, const uint64_t* legal,
+                  oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    const size_t E = (size_t)env->E, W = (size_t)env->W;
+    hipStream_t s = (hipStream_t)stream;
+    if (boards) OTH_HIP(hipMemcpyAsync(env->boards, boards, E * 2 * W * 8, hipMemcpyDefault, s));
+    if (meta) OTH_HIP(hipMemcpyAsync(env->meta, meta, E * 2, hipMemcpyDefault, s));
+    if (legal) OTH_HIP(hipMemcpyAsync(env->legal, legal, E * W * 8, hipMemcpyDefault, s));
+    return OTH_OK;
+}
+
+int oth_set_player_turn(oth_env* env, int32_t turn, const uint8_t* mask, oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    if (turn != WHITE_DISK && turn != BLACK_DISK) return fail(OTH_EINVAL, "turn must be +1 or -1");
+    return with_n(env->n, [&](auto NC) {
+        constexpr int N = decltype(NC)::value;
+        hipLaunchKernelGGL(k_set_turn<N>, dim3(grid_for(env->E)), dim3(BLOCK), 0, (hipStream_t)stream,
+                           env->boards, env->meta, env->legal, env->E, turn, mask);
+        return after_launch("oth_set_player_turn");
+    });
+}
+
+int oth_count_disks(oth_env* env, int32_t* out, oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    if (!out) return fail(OTH_EINVAL, "out is NULL");
+    return with_n(env->n, [&](auto NC) {
+        constexpr int N = decltype(NC)::value;
+        hipLaunchKernelGGL(k_count<N>, dim3(grid_for(env->E)), dim3(BLOCK), 0, (hipStream_t)stream, env->boards,
+                           env->E, out);
+        return after_launch("oth_count_disks");
+    });
+}
+
+int oth_counts(oth_env* env, int64_t* out, int32_t reset, oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    if (!out) return fail(OTH_EINVAL, "out is NULL");
+    hipStream_t s = (hipStream_t)stream;
+    OTH_HIP(hipMemcpyAsync(out, env->wdl, 3 * sizeof(int64_t), hipMemcpyDefault, s));
+    if (reset) OTH_HIP(hipMemsetAsync(env->wdl, 0, 4 * sizeof(unsigned long long), s));
+    return OTH_OK;
+}
+
+uint64_t oth_ply_counter(const oth_env* env) { return env ? env->ply : 0; }
+
+int oth_set_ply_counter(oth_env* env, uint64_t ply) {
+    if (!env) return fail(OTH_EINVAL, "NULL oth_env");
+    env->ply = ply;
+    return OTH_OK;
+}
+
+int oth_shape(const oth_env* env, int32_t* n_envs, int32_t* board_size, int32_t* words) {
+    if (!env) return fail(OTH_EINVAL, "NULL oth_env");
+    if (n_envs) *n_envs = env->E;
+    if (board_size) *board_size = env->n;
+    if (words) *words = env->W;
+    return OTH_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,70 @@
+"""Scripted policies with the reference's protocol (simple_policies.py).
+
+`reset(env)` (unwrapping `env.env` like simple_policies.py:28-32),
+`get_action(obs)`, `get_test_action(obs)`, optional `seed(seed)`.
+
+RandomPolicy draws exactly like simple_policies.py:37-41 (np.random.RandomState
+index into possible_moves), so seeded games match the reference move for move.
+GreedyPolicy asks the device kernel (oth_greedy_actions) for the move of
+simple_policies.py:69-92 -- the one flipping the most discs, lowest square on
+ties -- instead of simulating every candidate on a copied env.
+"""
+import numpy as np
+
+from .othello import WHITE_DISK
+
+PROTAGONIST_TURN = 1  # simple_policies.py:8-9
+OPPONENT_TURN = -1
+
+
+def _base(env):
+    return env.env if hasattr(env, 'env') else env
+
+
+class RandomPolicy(object):
+    """simple_policies.py:21-44"""
+
+    def __init__(self, seed=0):
+        self.rnd = np.random.RandomState(seed=seed)
+        self.env = None
+
+    def reset(self, env):
+        self.env = _base(env)
+
+    def seed(self, seed):
+        self.rnd = np.random.RandomState(seed=seed)
+
+    def get_action(self, obs):
+        possible_moves = self.env.possible_moves
+        ix = self.rnd.randint(0, len(possible_moves))
+        return possible_moves[ix]
+
+    def get_test_action(self, obs):
+        return self.get_action(obs)
+
+
+class GreedyPolicy(object):
+    """simple_policies.py:57-95, the candidate scan done by the k_greedy kernel."""
+
+    def __init__(self):
+        self.env = None
+
+    def reset(self, env):
+        self.env = _base(env)
+
+    def get_action(self, obs):
+        obs = np.asarray(obs)
+        if obs.ndim == 3 and obs.shape[0] == 4:  # make_state obs: same turn check as undo_state
+            assert int((self.env.player_turn + 1) / 2) == int(obs[2][0][0])
+        vec = self.env._vec
+        self.env._sync()
+        a = int(vec.greedy_actions().cpu()[0])
+        if a < 0:
+            raise ValueError('no possible moves')
+        return a
+
+    def get_test_action(self, obs):
+        return self.get_action(obs)
+
+
+__all__ = ['RandomPolicy', 'GreedyPolicy', 'PROTAGONIST_TURN', 'OPPONENT_TURN', 'WHITE_DISK']

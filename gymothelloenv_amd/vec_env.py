@@ -1,0 +1,248 @@
+"""VecOthelloEnv -- E Othello boards resident in HBM, stepped by HIP kernels.
+
+The batched form of the reference's OthelloBaseEnv (othello.py:217-501): one
+handle of the C ABI (include/othello_mi355x.h) owns E boards on one GPU; every
+method enqueues kernels on the current torch stream and returns torch tensors
+that stay on the device.  It replaces the reference's CPU "vector env" of one
+process per board (envs.py:7-287) for the hot path; torch here is only device
+memory, streams and the collective for the W/D/L tally.
+"""
+import ctypes
+
+import torch
+
+from . import _lib as L
+
+_OBS_LAYOUTS = {"board": L.OTH_OBS_BOARD, "board_legal": L.OTH_OBS_BOARD_LEGAL,
+                "make_state": L.OTH_OBS_MAKE_STATE, "absolute": L.OTH_OBS_ABSOLUTE}
+_OBS_PLANES = {L.OTH_OBS_BOARD: 1, L.OTH_OBS_BOARD_LEGAL: 2, L.OTH_OBS_MAKE_STATE: 4, L.OTH_OBS_ABSOLUTE: 1}
+_DTYPES = {torch.int8: L.OTH_I8, torch.int32: L.OTH_I32, torch.int64: L.OTH_I64,
+           torch.float32: L.OTH_F32, torch.float64: L.OTH_F64}
+_POLICIES = {"random": L.OTH_POLICY_RANDOM, "greedy": L.OTH_POLICY_GREEDY}
+
+BLACK_DISK, NO_DISK, WHITE_DISK = -1, 0, 1  # othello.py:10-12
+
+
+def nwords(n):
+    return (n * n + 63) // 64
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+class VecOthelloEnv(object):
+    """E independent boards of one size on one GPU.
+
+    Args mirror OthelloBaseEnv / SimpleOthelloEnv (othello.py:26-33, 222-227);
+    the batched extras are `auto_reset` (reset a board right after its terminal
+    ply), `seed` / `env_id_base` (Philox key and this shard's first global env
+    id) and `device`.
+    """
+
+    def __init__(self, num_envs, board_size=8, sudden_death_on_invalid_move=True,
+                 num_disk_as_reward=False, possible_actions_in_obs=False, auto_reset=False,
+                 initial_rand_steps=0, seed=0, env_id_base=0, device=None):
+        self._lib = L.load()
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device(device)
+        self.num_envs = int(num_envs)
+        self.board_size = max(4, int(board_size))  # othello.py:230
+        self.words = nwords(self.board_size)
+        self.sudden_death_on_invalid_move = bool(sudden_death_on_invalid_move)
+        self.num_disk_as_reward = bool(num_disk_as_reward)
+        self.possible_actions_in_obs = bool(possible_actions_in_obs)
+        self.auto_reset = bool(auto_reset)
+        self.initial_rand_steps = int(initial_rand_steps)
+        self.seed = int(seed)
+        self.env_id_base = int(env_id_base)
+        flags = ((L.OTH_SUDDEN_DEATH if self.sudden_death_on_invalid_move else 0) |
+                 (L.OTH_DISK_REWARD if self.num_disk_as_reward else 0) |
+                 (L.OTH_AUTO_RESET if self.auto_reset else 0))
+        self.flags = flags
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            L.check(self._lib.oth_create(self.num_envs, self.board_size, flags, self.seed & (2 ** 64 - 1),
+                                         self.env_id_base, self.initial_rand_steps, self.device.index,
+                                         ctypes.byref(h)), "oth_create")
+        self._h = h
+
+    # ------------------------------------------------------------------ utils
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.oth_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _i32(self, *shape):
+        return torch.empty(*shape, dtype=torch.int32, device=self.device)
+
+    def _u8(self, *shape):
+        return torch.empty(*shape, dtype=torch.uint8, device=self.device)
+
+    @property
+    def ply_counter(self):
+        return int(self._lib.oth_ply_counter(self._h))
+
+    @ply_counter.setter
+    def ply_counter(self, v):
+        L.check(self._lib.oth_set_ply_counter(self._h, int(v)), "oth_set_ply_counter")
+
+    # ---------------------------------------------------------------- the API
+    def reset(self, mask=None):
+        """OthelloBaseEnv.reset (othello.py:265-271) for every board (or where mask)."""
+        m = None
+        if mask is not None:
+            m = mask.to(device=self.device, dtype=torch.uint8).contiguous()
+        L.check(self._lib.oth_reset(self._h, _ptr(m), self._stream()), "oth_reset")
+        return self.get_observation()
+
+    def step(self, actions, rewards=None, dones=None, observe=True):
+        """OthelloBaseEnv.step (othello.py:412-462) on every board.
+
+        actions: int tensor (E,).  Returns (obs, rewards int32 (E,), dones bool (E,), None)
+        -- obs is None when observe=False."""
+        a = actions.to(device=self.device, dtype=torch.int32).contiguous()
+        if a.numel() != self.num_envs:
+            raise ValueError("expected %d actions, got %d" % (self.num_envs, a.numel()))
+        r = rewards if rewards is not None else self._i32(self.num_envs)
+        d = dones if dones is not None else self._u8(self.num_envs)
+        L.check(self._lib.oth_step(self._h, _ptr(a), _ptr(r), _ptr(d), self._stream()), "oth_step")
+        obs = self.get_observation() if observe else None
+        return obs, r, d.bool(), None
+
+    def step_policy(self, policy="random", n_plies=1, actions=None, rewards=None, dones=None, record=True):
+        """n_plies plies where every board's mover plays `policy` on the device
+        (RandomPolicy simple_policies.py:37-41 / GreedyPolicy :69-92).
+
+        Returns (actions, rewards, dones) of shape (n_plies, E) (None if not recorded)."""
+        pol = _POLICIES[policy] if isinstance(policy, str) else int(policy)
+        if record:
+            actions = actions if actions is not None else self._i32(n_plies, self.num_envs)
+            rewards = rewards if rewards is not None else self._i32(n_plies, self.num_envs)
+            dones = dones if dones is not None else self._u8(n_plies, self.num_envs)
+        L.check(self._lib.oth_step_policy(self._h, pol, int(n_plies), _ptr(actions), _ptr(rewards),
+                                          _ptr(dones), self._stream()), "oth_step_policy")
+        return actions, rewards, dones
+
+    def legal_mask(self):
+        """possible_moves of every board as (E, W) int64 bit masks (bit a = square a)."""
+        out = torch.empty(self.num_envs, self.words, dtype=torch.int64, device=self.device)
+        L.check(self._lib.oth_legal(self._h, _ptr(out), self._stream()), "oth_legal")
+        return out
+
+    def legal_actions(self):
+        """possible_moves as a bool (E, N*N) tensor (the obs legal plane, unconditioned)."""
+        o = self.observe("board_legal", torch.int8)
+        return o[:, 1].reshape(self.num_envs, -1).bool()
+
+    def greedy_actions(self):
+        out = self._i32(self.num_envs)
+        L.check(self._lib.oth_greedy_actions(self._h, _ptr(out), self._stream()), "oth_greedy_actions")
+        return out
+
+    def observe(self, layout="board", dtype=torch.int64, out=None):
+        lay = _OBS_LAYOUTS[layout] if isinstance(layout, str) else int(layout)
+        planes = _OBS_PLANES[lay]
+        n = self.board_size
+        shape = (self.num_envs, n, n) if lay in (L.OTH_OBS_BOARD, L.OTH_OBS_ABSOLUTE) else \
+            (self.num_envs, planes, n, n)
+        if out is None:
+            out = torch.empty(shape, dtype=dtype, device=self.device)
+        L.check(self._lib.oth_observe(self._h, lay, _DTYPES[out.dtype], _ptr(out), self._stream()),
+                "oth_observe")
+        return out
+
+    def get_observation(self, dtype=torch.int64):
+        """get_observation (othello.py:363-378): mover-perspective board, plus the
+        possible-moves plane when possible_actions_in_obs."""
+        return self.observe("board_legal" if self.possible_actions_in_obs else "board", dtype)
+
+    def make_state(self, dtype=torch.float32):
+        """util.make_state (util.py:48-74) for every board: (E, 4, N, N)."""
+        return self.observe("make_state", dtype)
+
+    def count_disks(self):
+        """count_disks (othello.py:468-471): int32 (E, 2) = (white_cnt, black_cnt)."""
+        out = self._i32(self.num_envs, 2)
+        L.check(self._lib.oth_count_disks(self._h, _ptr(out), self._stream()), "oth_count_disks")
+        return out
+
+    def set_player_turn(self, turn, mask=None):
+        """set_player_turn (othello.py:464-466): set the turn and recompute possible_moves."""
+        m = None if mask is None else mask.to(device=self.device, dtype=torch.uint8).contiguous()
+        L.check(self._lib.oth_set_player_turn(self._h, int(turn), _ptr(m), self._stream()),
+                "oth_set_player_turn")
+
+    def get_state(self):
+        """(boards (E, 2W) int64, meta (E,) int16, legal (E, W) int64) device copies
+        in the exchange format of include/othello_mi355x.h."""
+        b = torch.empty(self.num_envs, 2 * self.words, dtype=torch.int64, device=self.device)
+        m = torch.empty(self.num_envs, dtype=torch.int16, device=self.device)
+        lg = torch.empty(self.num_envs, self.words, dtype=torch.int64, device=self.device)
+        L.check(self._lib.oth_get_state(self._h, _ptr(b), _ptr(m), _ptr(lg), self._stream()), "oth_get_state")
+        return b, m, lg
+
+    def set_state(self, boards=None, meta=None, legal=None):
+        def dev(t, dt):
+            return None if t is None else t.to(device=self.device).contiguous().view(dt)
+        b, m, lg = dev(boards, torch.int64), dev(meta, torch.int16), dev(legal, torch.int64)
+        for t, per in ((b, 2 * self.words), (m, 1), (lg, self.words)):
+            if t is not None and t.numel() != self.num_envs * per:
+                raise ValueError("state tensor has %d elements, expected %d" % (t.numel(), self.num_envs * per))
+        L.check(self._lib.oth_set_state(self._h, _ptr(b), _ptr(m), _ptr(lg), self._stream()), "oth_set_state")
+        # keep the sources alive until the async copies ran
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def counts(self, reset=False):
+        """{black wins, draws, white wins} of games finished since the last reset (int64 (3,))."""
+        out = torch.empty(3, dtype=torch.int64, device=self.device)
+        L.check(self._lib.oth_counts(self._h, _ptr(out), int(bool(reset)), self._stream()), "oth_counts")
+        return out
+
+    def state_dict(self):
+        b, m, lg = self.get_state()
+        return {"boards": b, "meta": m, "legal": lg, "ply_counter": self.ply_counter,
+                "board_size": self.board_size, "num_envs": self.num_envs}
+
+    def load_state_dict(self, sd):
+        if sd["board_size"] != self.board_size or sd["num_envs"] != self.num_envs:
+            raise ValueError("state_dict shape does not match this env")
+        self.set_state(sd["boards"], sd["meta"], sd["legal"])
+        self.ply_counter = sd["ply_counter"]
+
+    # decoded views of the meta word
+    def player_turn(self):
+        b, m, _ = self.get_state()
+        return torch.where((m & 1) != 0, WHITE_DISK, BLACK_DISK)
+
+    def terminated(self):
+        _, m, _ = self.get_state()
+        return ((m >> 1) & 1) != 0
+
+    def winner(self):
+        _, m, _ = self.get_state()
+        w = (m >> 2) & 3
+        return torch.where(w == 1, WHITE_DISK, torch.where(w == 2, BLACK_DISK, NO_DISK))
+
+
+def legal_moves(board_size, mover, opponent):
+    """Stateless get_possible_actions(board) (othello.py:313-343) on canonical
+    boards given as (n, W) int64 mover / opponent masks on a GPU."""
+    lib = L.load()
+    mover = mover.contiguous()
+    opponent = opponent.to(mover.device).contiguous()
+    out = torch.empty_like(mover)
+    stream = ctypes.c_void_p(torch.cuda.current_stream(mover.device).cuda_stream)
+    L.check(lib.oth_legal_moves(int(board_size), int(mover.shape[0]), _ptr(mover), _ptr(opponent), _ptr(out),
+                                stream), "oth_legal_moves")
+    return out

@@ -1,0 +1,150 @@
+/*
+ * othello_mi355x.h -- C ABI of the MI355X-native vectorised Othello rules engine.
+ *
+ * Drop-in boundary for the reference's hot path: the
+ * in-process Gym-style API of OthelloBaseEnv / SimpleOthelloEnv / OthelloEnv
+ * (othello.py:21-501), batched over E boards that live in HBM.  The reference
+ * is pure Python and has no FFI of its own, so these entry points are what a
+ * ctypes binding of it would call (INTEGRATION.md shows that binding).
+ *
+ * Each entry point below names the reference function it replaces.
+ *
+ * Conventions
+ *   - All array arguments are DEVICE pointers (hipMalloc / torch.cuda tensors)
+ *     unless stated; `stream` is a hipStream_t (NULL = the null stream).  Calls
+ *     only enqueue work: nothing synchronises the host.
+ *   - Square a = row * N + col (othello.py:392-393); action a in [0, N*N).
+ *   - W = ceil(N*N / 64) 64-bit words per colour (1 for N <= 8, up to 4 for N = 16).
+ *   - State exchange format (also used by the test oracle):
+ *       boards  uint64[E][2W]  words 0..W-1 black discs, W..2W-1 white discs
+ *       meta    uint16[E]      bit0 white to move (player_turn == WHITE_DISK)
+ *                              bit1 terminated
+ *                              bits2-3 winner: 0 NO_DISK / draw, 1 WHITE, 2 BLACK
+ *                              bits8-15 random-opening plies still to play
+ *       legal   uint64[E][W]   possible_moves -- NOT recomputed on terminal
+ *                              plies, exactly like the reference (othello.py:431-433)
+ *   - Return value: OTH_OK (0) or a negative OTH_E* code; oth_last_error()
+ *     gives the message for the calling thread.
+ *   - A handle is bound to one device; calls on one handle must be serialised
+ *     by the caller.  Separate handles are independent.
+ */
+#ifndef OTHELLO_MI355X_H
+#define OTHELLO_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct oth_env oth_env;
+typedef void *oth_stream_t; /* hipStream_t */
+
+enum {
+    OTH_OK = 0,
+    OTH_EINVAL = -1, /* bad argument (board size outside [4,16], NULL pointer, ...) */
+    OTH_EHIP = -2,   /* a HIP runtime call failed */
+    OTH_ENOMEM = -3
+};
+
+/* create flags: the reference's constructor switches (othello.py:222-227) */
+enum {
+    OTH_SUDDEN_DEATH = 1, /* sudden_death_on_invalid_move */
+    OTH_DISK_REWARD = 2,  /* num_disk_as_reward */
+    OTH_AUTO_RESET = 4    /* batched only: reset an env right after its terminal ply */
+};
+
+enum { OTH_POLICY_RANDOM = 0, OTH_POLICY_GREEDY = 1 };
+
+/* observation layouts */
+enum {
+    OTH_OBS_BOARD = 0,       /* (E,N,N)   get_observation(): mover +1, opponent -1 (othello.py:363-369) */
+    OTH_OBS_BOARD_LEGAL = 1, /* (E,2,N,N) get_observation() with possible_actions_in_obs (othello.py:370-376) */
+    OTH_OBS_MAKE_STATE = 2,  /* (E,4,N,N) util.make_state(obs, env) planes (util.py:48-74) */
+    OTH_OBS_ABSOLUTE = 3     /* (E,N,N)   board_state: white +1, black -1 (othello.py:257) */
+};
+/* observation element types */
+enum { OTH_I8 = 0, OTH_I32 = 1, OTH_I64 = 2, OTH_F32 = 3, OTH_F64 = 4 };
+
+/* OthelloBaseEnv.__init__ (othello.py:222-254) for n_envs boards of size
+ * board_size (clamped to >= 4 like othello.py:230; > 16 is OTH_EINVAL).
+ * seed / env_id_base key the Philox RNG of the on-device policies: env i uses
+ * id env_id_base + i, so a sharded run reproduces an unsharded one.
+ * initial_rand_steps: SimpleOthelloEnv's random-opening length bound
+ * (othello.py:62-63) applied by oth_reset and auto-reset.  Boards start reset. */
+int oth_create(int32_t n_envs, int32_t board_size, uint32_t flags, uint64_t seed, uint32_t env_id_base,
+               int32_t initial_rand_steps, int32_t device, oth_env **out);
+int oth_destroy(oth_env *env);
+
+/* OthelloBaseEnv.reset (othello.py:265-271) for every env, or only where
+ * mask[e] != 0 (mask: device uint8[E] or NULL). */
+int oth_reset(oth_env *env, const uint8_t *mask, oth_stream_t stream);
+
+/* OthelloBaseEnv.step (othello.py:412-462) with external actions int32[E].
+ * Out: rewards int32[E], dones uint8[E] (either may be NULL).  An env that is
+ * already terminated is left unchanged and reports done = 1, reward = 0 (the
+ * reference raises ValueError there, othello.py:415-416; the single-env
+ * wrapper does so on the host). */
+int oth_step(oth_env *env, const int32_t *actions, int32_t *rewards, uint8_t *dones, oth_stream_t stream);
+
+/* n_plies plies of on-device play: each env's mover picks with `policy`
+ * (RandomPolicy.get_action simple_policies.py:37-41 / GreedyPolicy.get_action
+ * :69-92, or a random move while random-opening plies remain) and steps.
+ * Outputs are [n_plies][E] (any may be NULL): the action played (-1 for an
+ * env that was already terminated), reward, done.  Finished games are tallied
+ * into the handle's win/draw/loss counters (oth_counts). */
+int oth_step_policy(oth_env *env, int32_t policy, int32_t n_plies, int32_t *actions, int32_t *rewards,
+                    uint8_t *dones, oth_stream_t stream);
+
+/* possible_moves of every env as masks uint64[E][W] (othello.py:242, :270, :466). */
+int oth_legal(oth_env *env, uint64_t *out, oth_stream_t stream);
+
+/* get_possible_actions(board) (othello.py:313-343), stateless: n canonical
+ * boards given as mover / opponent masks uint64[n][W] -> uint64[n][W]. */
+int oth_legal_moves(int32_t board_size, int32_t n, const uint64_t *mover, const uint64_t *opp, uint64_t *out,
+                    oth_stream_t stream);
+
+/* GreedyPolicy.get_action (simple_policies.py:69-92) for the side to move in
+ * every env: argmax over possible_moves of the discs flipped, lowest square
+ * on ties; -1 where possible_moves is empty.  Out int32[E]. */
+int oth_greedy_actions(oth_env *env, int32_t *out, oth_stream_t stream);
+
+/* Observations: layout OTH_OBS_*, dtype OTH_I8..OTH_F64, out (E, planes, N, N). */
+int oth_observe(oth_env *env, int32_t layout, int32_t dtype, void *out, oth_stream_t stream);
+
+/* Copy the state out / in (exchange format above).  In oth_set_state any of
+ * the three sources may be NULL (left unchanged): set_board_state
+ * (othello.py:380-389) replaces only the boards. */
+int oth_get_state(oth_env *env, uint64_t *boards, uint16_t *meta, uint64_t *legal, oth_stream_t stream);
+int oth_set_state(oth_env *env, const uint64_t *boards, const uint16_t *meta, const uint64_t *legal,
+                  oth_stream_t stream);
+
+/* set_player_turn (othello.py:464-466): turn (+1 white / -1 black) for every
+ * env (or where mask[e] != 0), then recompute possible_moves. */
+int oth_set_player_turn(oth_env *env, int32_t turn, const uint8_t *mask, oth_stream_t stream);
+
+/* count_disks (othello.py:468-471): out int32[E][2] = (white_cnt, black_cnt). */
+int oth_count_disks(oth_env *env, int32_t *out, oth_stream_t stream);
+
+/* Win/draw/loss tally of games finished by oth_step / oth_step_policy since
+ * the last reset of the counters: out int64[3] = {black wins, draws, white
+ * wins} (device pointer).  reset != 0 zeroes the counters after the copy. */
+int oth_counts(oth_env *env, int64_t *out, int32_t reset, oth_stream_t stream);
+
+/* Global ply counter of the handle (the Philox counter of the next ply). */
+uint64_t oth_ply_counter(const oth_env *env);
+int oth_set_ply_counter(oth_env *env, uint64_t ply);
+
+/* Handle geometry: n_envs, board_size, W. */
+int oth_shape(const oth_env *env, int32_t *n_envs, int32_t *board_size, int32_t *words);
+
+/* Message of the last failing call on this thread ("" if none). */
+const char *oth_last_error(void);
+
+/* Library version string. */
+const char *oth_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OTHELLO_MI355X_H */

@@ -37,7 +37,7 @@ def lib():
         L.oracle_nwords.argtypes = [i32]
         L.oracle_reset_batch.argtypes = [i32, i32, P, P, P]
         L.oracle_legal_batch.argtypes = [i32, i32, P, P, P]
-        L.oracle_step_batch.argtypes = [i32, u32, i32, P, P, P, P, P, P]
+        L.oracle_step_batch.argtypes = [i32, u32, u64, u32, u64, i32, i32, P, P, P, P, P, P, P]
         L.oracle_step_batch.restype = i32
         L.oracle_reset_openings.argtypes = [i32, i32, u64, u32, u64, i32, P, P, P]
         L.oracle_rollout.argtypes = [i32, u32, i32, i32, u64, u32, u64, i32, i32, P, P, P, P, P, P, P]
@@ -96,13 +96,15 @@ def legal(n, mover, opp):
     return out
 
 
-def step(s, flags, actions):
-    """In-place step of State s; returns (rewards, dones, n_stepped_while_terminated)."""
+def step(s, flags, actions, seed=0, id_base=0, ply=0, initial_rand_steps=0, wdl=None):
+    """In-place step of State s; returns (rewards, dones, n_stepped_while_terminated).
+    wdl: optional int64[3] accumulator {black wins, draws, white wins}."""
     actions = np.ascontiguousarray(actions, dtype=np.int32)
     rewards = np.zeros(s.E, dtype=np.int32)
     dones = np.zeros(s.E, dtype=np.uint8)
-    errs = lib().oracle_step_batch(s.n, flags, s.E, _p(s.boards), _p(s.meta), _p(s.legal),
-                                   _p(actions), _p(rewards), _p(dones))
+    errs = lib().oracle_step_batch(s.n, flags, seed, id_base, ply, initial_rand_steps, s.E,
+                                   _p(s.boards), _p(s.meta), _p(s.legal), _p(actions), _p(rewards),
+                                   _p(dones), _p(wdl))
     return rewards, dones, errs
 
 

@@ -312,10 +312,14 @@ void oracle_legal_batch(int n, int E, const uint64_t *mover, const uint64_t *opp
 /* OthelloBaseEnv.step (othello.py:412-462) for E envs with external actions.
  * A terminated env is left unchanged and reports done=1, reward=0 (the batched
  * stand-in for the reference's ValueError); with F_AUTO_RESET an env that
- * terminates is reset after its outputs are written.  Returns the number of
- * envs that were stepped while already terminated. */
-int oracle_step_batch(int n, uint32_t flags, int E, uint64_t *boards, uint16_t *meta, uint64_t *legal,
-                      const int32_t *actions, int32_t *rewards, uint8_t *dones) {
+ * terminates is reset after its outputs are written (random-opening length
+ * drawn with purpose 1 at ply `ply`).  Games that end are tallied into wdl
+ * (may be NULL).  Returns the number of envs stepped while already terminated. */
+static int opening_plies(uint64_t seed, uint32_t id, uint64_t ply, uint32_t purpose, int initial_rand_steps);
+
+int oracle_step_batch(int n, uint32_t flags, uint64_t seed, uint32_t id_base, uint64_t ply, int initial_rand_steps,
+                      int E, uint64_t *boards, uint16_t *meta, uint64_t *legal, const int32_t *actions,
+                      int32_t *rewards, uint8_t *dones, int64_t *wdl) {
     int W = nwords(n), errs = 0;
     oenv e;
     for (int i = 0; i < E; i++) {
@@ -326,10 +330,14 @@ int oracle_step_batch(int n, uint32_t flags, int E, uint64_t *boards, uint16_t *
             errs++;
             r = 0;
             d = 1;
-        } else if (d && (flags & F_AUTO_RESET)) {
-            int keep = e.rand_left;
-            env_reset(&e);
-            e.rand_left = keep;
+        } else if (d) {
+            if (wdl) wdl[e.winner == BLACK_DISK ? 0 : (e.winner == NO_DISK ? 1 : 2)]++;
+            if (flags & F_AUTO_RESET) {
+                env_reset(&e);
+                e.rand_left = initial_rand_steps > 0
+                                  ? opening_plies(seed, id_base + (uint32_t)i, ply, 1, initial_rand_steps)
+                                  : 0;
+            }
         }
         rewards[i] = r;
         dones[i] = (uint8_t)d;

@@ -1,0 +1,93 @@
+"""CPU-side checks of the boundary: the in-tree HIP library loads and exports
+every entry point include/othello_mi355x.h declares (no compute calls -- there
+is no GPU here), and the host-side conversions of the drop-in layer."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "othello_mi355x.h")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(oth_[a-z_]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from gymothelloenv_amd import _lib
+    from gymothelloenv_amd import build as hb
+    if hb.needs_build():
+        hb.build()
+    return _lib.load(require_gpu=False)
+
+
+def test_library_exports_every_declared_symbol(lib):
+    from gymothelloenv_amd import _lib
+    syms = declared_symbols()
+    assert len(syms) >= 18
+    for s in syms:
+        assert hasattr(lib, s), s
+        assert s in _lib.SIGNATURES, s
+    assert set(_lib.SIGNATURES) == set(syms)
+    assert b"gfx950" in lib.oth_version()
+    assert lib.oth_last_error() == b""
+
+
+def test_library_is_gfx950_code_object():
+    from gymothelloenv_amd import _lib
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+    assert b"gfx942" not in blob and b"sm_" not in blob[:0]
+
+
+def test_invalid_arguments_fail_without_gpu(lib):
+    import ctypes
+    h = ctypes.c_void_p()
+    assert lib.oth_create(0, 8, 0, 0, 0, 0, 0, ctypes.byref(h)) == -1
+    assert b"n_envs" in lib.oth_last_error()
+    assert lib.oth_create(16, 17, 0, 0, 0, 0, 0, ctypes.byref(h)) == -1
+    assert lib.oth_create(16, 8, 8, 0, 0, 0, 0, ctypes.byref(h)) == -1
+    assert lib.oth_reset(None, None, None) == -1
+    assert lib.oth_legal_moves(8, -1, None, None, None, None) == -1
+    assert lib.oth_legal_moves(8, 0, None, None, None, None) == 0
+
+
+def test_mask_conversions():
+    from gymothelloenv_amd.othello import _board_to_masks, _list_to_mask, _mask_to_list
+    for n in (4, 8, 10, 16):
+        moves = sorted(np.random.RandomState(n).choice(n * n, size=n, replace=False).tolist())
+        m = _list_to_mask(moves, n)
+        assert m.dtype == np.int64 and m.shape == ((n * n + 63) // 64,)
+        assert _mask_to_list(m.view(np.uint64), n * n) == moves
+        board = np.zeros((n, n), dtype=int)
+        board.ravel()[moves[: n // 2]] = 1
+        board.ravel()[moves[n // 2:]] = -1
+        plus, minus = _board_to_masks(board, n)
+        assert _mask_to_list(plus.view(np.uint64), n * n) == moves[: n // 2]
+        assert _mask_to_list(minus.view(np.uint64), n * n) == moves[n // 2:]
+
+
+def test_spaces():
+    from gymothelloenv_amd.spaces import Box, Discrete
+    d = Discrete(64)
+    assert d.n == 64 and d.contains(63) and not d.contains(64)
+    b = Box(np.zeros([2, 8, 8]), np.ones([2, 8, 8]))
+    assert b.shape == (2, 8, 8) and b.contains(np.zeros((2, 8, 8)))
+
+
+def test_product_has_no_cpu_fallback():
+    """The product package never imports the oracle, and refuses to run without a GPU."""
+    pkg = os.path.join(ROOT, "gymothelloenv_amd")
+    for fn in os.listdir(pkg):
+        if fn.endswith(".py"):
+            assert "oracle" not in open(os.path.join(pkg, fn)).read().replace("oracle/", ""), fn
+    import torch
+    if not torch.cuda.is_available():
+        from gymothelloenv_amd import OthelloLibError, VecOthelloEnv
+        with pytest.raises(OthelloLibError):
+            VecOthelloEnv(4)

@@ -1,0 +1,296 @@
+"""GPU parity: the HIP engine (through the C ABI) against the reference's golden
+fixtures and the CPU oracle, bit for bit.  Run on an MI355X (`-m gpu`)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+SIZES = list(range(4, 17))
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def t64(torch, a):
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).cuda()
+
+
+def np_u64(t):
+    return t.cpu().numpy().view(np.uint64)
+
+
+def flags_of(sd, dr, auto=False):
+    return ((oracle.F_SUDDEN_DEATH if sd else 0) | (oracle.F_DISK_REWARD if dr else 0) |
+            (oracle.F_AUTO_RESET if auto else 0))
+
+
+def make_env(torch, E, n, sd=True, dr=False, auto=False, seed=0, id_base=0, init_rand=0):
+    from gymothelloenv_amd import VecOthelloEnv
+    return VecOthelloEnv(E, board_size=n, sudden_death_on_invalid_move=sd, num_disk_as_reward=dr,
+                         auto_reset=auto, seed=seed, env_id_base=id_base, initial_rand_steps=init_rand,
+                         device="cuda:0")
+
+
+def get_state_np(env):
+    b, m, lg = env.get_state()
+    return np_u64(b), m.cpu().numpy().view(np.uint16), np_u64(lg)
+
+
+def test_kat(torch_cuda, golden_dir):
+    torch = torch_cuda
+    kat = json.load(open(os.path.join(golden_dir, "kat.json")))
+    for n in SIZES:
+        k = kat[str(n)]
+        env = make_env(torch, 3, n)
+        b, m, lg = get_state_np(env)
+        W = oracle.nwords(n)
+        for e in range(3):
+            assert list(b[e, :W]) == k["black"] and list(b[e, W:]) == k["white"]
+            moves = [a for a in range(n * n) if (int(lg[e, a // 64]) >> (a % 64)) & 1]
+            assert moves == k["black_moves"]
+        env.step(torch.full((3,), k["black_moves"][0], dtype=torch.int32))
+        _, _, lg = get_state_np(env)
+        moves = [a for a in range(n * n) if (int(lg[0, a // 64]) >> (a % 64)) & 1]
+        assert moves == k["white_moves_after_lowest"]
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_step_matches_reference_golden(torch_cuda, golden_dir, n):
+    """Every ply the reference recorded, stepped on the GPU from its pre-state."""
+    torch = torch_cuda
+    t = dict(np.load(os.path.join(golden_dir, "traj_N%d.npz" % n)))
+    for ci, (sd, dr) in enumerate(t["combos"]):
+        sel = t["combo"] == ci
+        E = int(sel.sum())
+        env = make_env(torch, E, n, sd=bool(sd), dr=bool(dr))
+        env.set_state(t64(torch, np.concatenate([t["prev_black"][sel], t["prev_white"][sel]], axis=1)),
+                      torch.from_numpy(oracle.meta_from(t["prev_turn"][sel]).view(np.int16)).cuda(),
+                      t64(torch, t["prev_legal"][sel]))
+        _, rew, dones, _ = env.step(torch.from_numpy(t["action"][sel]).cuda())
+        b, m, lg = get_state_np(env)
+        np.testing.assert_array_equal(b, np.concatenate([t["black"][sel], t["white"][sel]], axis=1))
+        np.testing.assert_array_equal(lg, t["legal"][sel])
+        np.testing.assert_array_equal(rew.cpu().numpy(), t["reward"][sel])
+        np.testing.assert_array_equal(dones.cpu().numpy(), t["done"][sel])
+        np.testing.assert_array_equal(np.where(m & 1, 1, -1), t["turn"][sel])
+        wc = (m >> 2) & 3
+        np.testing.assert_array_equal(np.where(wc == 1, 1, np.where(wc == 2, -1, 0)), t["winner"][sel])
+        env.close()
+
+
+@pytest.mark.parametrize("n", [4, 5, 8, 10, 16])
+def test_games_in_lockstep(torch_cuda, golden_dir, n):
+    """All recorded games of a combo advance together from reset, one GPU step
+    per ply; finished games are masked with an (ignored) action."""
+    torch = torch_cuda
+    t = dict(np.load(os.path.join(golden_dir, "traj_N%d.npz" % n)))
+    for ci, (sd, dr) in enumerate(t["combos"]):
+        games = np.unique(t["game"][t["combo"] == ci])
+        env = make_env(torch, len(games), n, sd=bool(sd), dr=bool(dr))
+        idx = [np.flatnonzero((t["combo"] == ci) & (t["game"] == g)) for g in games]
+        for p in range(max(len(i) for i in idx)):
+            acts = np.array([t["action"][i[p]] if p < len(i) else 0 for i in idx], dtype=np.int32)
+            _, rew, dn, _ = env.step(torch.from_numpy(acts).cuda())
+            b, _, lg = get_state_np(env)
+            rew, dn = rew.cpu().numpy(), dn.cpu().numpy()
+            for gi, i in enumerate(idx):
+                if p < len(i):
+                    k = i[p]
+                    assert rew[gi] == t["reward"][k] and dn[gi] == t["done"][k]
+                    assert list(b[gi]) == list(t["black"][k]) + list(t["white"][k])
+                    assert list(lg[gi]) == list(t["legal"][k])
+                else:  # past the end: stepping a terminated game is a no-op reporting done
+                    assert dn[gi] == 1 and rew[gi] == 0
+
+
+@pytest.mark.parametrize("n,E,plies", [(8, 65536, 130), (6, 16384, 80), (10, 8192, 200), (16, 1024, 260)])
+def test_random_rollout_replays_on_oracle(torch_cuda, n, E, plies):
+    """Config 2 / 5: on-device random play with auto-reset; every action, reward,
+    done, the final state and the W/D/L tally equal the oracle's replay."""
+    torch = torch_cuda
+    env = make_env(torch, E, n, auto=True, seed=7)
+    acts, rews, dones = env.step_policy("random", n_plies=plies)
+    b, m, lg = get_state_np(env)
+    wdl = env.counts().cpu().numpy()
+    s = oracle.reset(n, E)
+    oa, orw, od, owdl = oracle.rollout(s, flags_of(True, False, True), 0, plies, seed=7)
+    np.testing.assert_array_equal(acts.cpu().numpy(), oa)
+    np.testing.assert_array_equal(rews.cpu().numpy(), orw)
+    np.testing.assert_array_equal(dones.cpu().numpy(), od)
+    np.testing.assert_array_equal(b, s.boards)
+    np.testing.assert_array_equal(m, s.meta)
+    np.testing.assert_array_equal(lg, s.legal)
+    np.testing.assert_array_equal(wdl, owdl)
+    assert owdl.sum() >= E  # at least one finished game per board
+
+
+def test_rollout_split_over_launches_is_identical(torch_cuda):
+    """K plies in one launch == K single-ply launches (state round-trips HBM)."""
+    torch = torch_cuda
+    a = make_env(torch, 4096, 8, auto=True, seed=3)
+    b = make_env(torch, 4096, 8, auto=True, seed=3)
+    acts_a, _, _ = a.step_policy("random", n_plies=90)
+    acts_b = torch.cat([b.step_policy("random", n_plies=1)[0] for _ in range(90)])
+    assert torch.equal(acts_a, acts_b)
+    for x, y in zip(a.get_state(), b.get_state()):
+        assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("n,init_rand", [(8, 10), (6, 4)])
+def test_greedy_rollout_replays_on_oracle(torch_cuda, n, init_rand):
+    """Config 3: greedy vs greedy after Philox random openings (0..init_rand plies)."""
+    torch = torch_cuda
+    E, plies = 2048, 140
+    env = make_env(torch, E, n, auto=True, seed=11, init_rand=init_rand)
+    env.reset()
+    acts, rews, dones = env.step_policy("greedy", n_plies=plies)
+    b, m, lg = get_state_np(env)
+    s = oracle.reset_openings(n, E, 11, 0, 0, init_rand)
+    oa, orw, od, owdl = oracle.rollout(s, flags_of(True, False, True), 1, plies, seed=11,
+                                       initial_rand_steps=init_rand)
+    np.testing.assert_array_equal(acts.cpu().numpy(), oa)
+    np.testing.assert_array_equal(rews.cpu().numpy(), orw)
+    np.testing.assert_array_equal(dones.cpu().numpy(), od)
+    np.testing.assert_array_equal(b, s.boards)
+    np.testing.assert_array_equal(m, s.meta)
+    np.testing.assert_array_equal(env.counts().cpu().numpy(), owdl)
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_greedy_actions_match_reference(torch_cuda, golden_dir, n):
+    torch = torch_cuda
+    g = np.load(os.path.join(golden_dir, "greedy.npz"))
+    b, w, t, a = g["N%d_black" % n], g["N%d_white" % n], g["N%d_turn" % n], g["N%d_action" % n]
+    env = make_env(torch, len(a), n)
+    env.set_state(t64(torch, np.concatenate([b, w], axis=1)),
+                  torch.from_numpy(oracle.meta_from(t).view(np.int16)).cuda())
+    env.set_player_turn(1, mask=torch.from_numpy((t == 1).astype(np.uint8)).cuda())
+    env.set_player_turn(-1, mask=torch.from_numpy((t == -1).astype(np.uint8)).cuda())
+    np.testing.assert_array_equal(env.greedy_actions().cpu().numpy(), a)
+
+
+def legal_bool(legal, n):
+    a = np.arange(n * n)
+    return ((legal[:, a // 64] >> (a % 64).astype(np.uint64)) & np.uint64(1)).astype(bool)
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_external_steps_with_invalid_actions(torch_cuda, n):
+    """Random external actions (legal, illegal, out of range) in all flag combos,
+    with auto-reset, against the oracle for 2*N*N plies."""
+    torch = torch_cuda
+    E = 1024
+    rng = np.random.RandomState(n)
+    for sd in (True, False):
+        for dr in (False, True):
+            env = make_env(torch, E, n, sd=sd, dr=dr, auto=True, seed=5)
+            s = oracle.reset(n, E)
+            wdl = np.zeros(3, dtype=np.int64)
+            for p in range(2 * n * n):
+                lb = legal_bool(s.legal, n)
+                pick = np.argmax(rng.rand(E, n * n) * lb, axis=1).astype(np.int32)
+                wild = (rng.rand(E) < 0.05) | ~lb.any(axis=1)
+                acts = np.where(wild, rng.randint(-2, n * n + 2, size=E), pick).astype(np.int32)
+                orw, od, _ = oracle.step(s, flags_of(sd, dr, True), acts, seed=5, ply=p, wdl=wdl)
+                _, rew, dn, _ = env.step(torch.from_numpy(acts).cuda(), observe=False)
+                np.testing.assert_array_equal(rew.cpu().numpy(), orw)
+                np.testing.assert_array_equal(dn.cpu().numpy(), od.astype(bool))
+            b, m, lg = get_state_np(env)
+            np.testing.assert_array_equal(b, s.boards)
+            np.testing.assert_array_equal(m, s.meta)
+            np.testing.assert_array_equal(lg, s.legal)
+            np.testing.assert_array_equal(env.counts().cpu().numpy(), wdl)
+
+
+@pytest.mark.parametrize("n", [6, 8])
+def test_observations_match_reference(torch_cuda, golden_dir, n):
+    torch = torch_cuda
+    o = np.load(os.path.join(golden_dir, "obs.npz"))
+    E = len(o["N%d_turn" % n])
+    env = make_env(torch, E, n)
+    env.set_state(t64(torch, np.concatenate([o["N%d_black" % n], o["N%d_white" % n]], axis=1)),
+                  torch.from_numpy(oracle.meta_from(o["N%d_turn" % n]).view(np.int16)).cuda(),
+                  t64(torch, o["N%d_legal" % n]))
+    for dt in (torch.int8, torch.int32, torch.int64, torch.float32, torch.float64):
+        np.testing.assert_array_equal(env.observe("board", dt).cpu().numpy(), o["N%d_obs" % n])
+        np.testing.assert_array_equal(env.observe("board_legal", dt).cpu().numpy(), o["N%d_obs2" % n])
+        np.testing.assert_array_equal(env.observe("make_state", dt).cpu().numpy(), o["N%d_make_state" % n])
+    ab = env.observe("absolute", torch.int64).cpu().numpy()
+    W = oracle.nwords(n)
+    bl = o["N%d_black" % n]
+    for e in range(0, E, 97):
+        for a in range(n * n):
+            isb = (int(bl[e, a // 64]) >> (a % 64)) & 1
+            assert ab[e].ravel()[a] == (-1 if isb else (1 if (int(o["N%d_white" % n][e, a // 64]) >> (a % 64)) & 1
+                                                         else 0))
+    assert W >= 1
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_stateless_legal_moves(torch_cuda, n):
+    torch = torch_cuda
+    from gymothelloenv_amd import legal_moves
+    rng = np.random.RandomState(100 + n)
+    E, W = 4096, oracle.nwords(n)
+    cells = rng.randint(0, 3, size=(E, n * n))
+    mover = np.zeros((E, W), dtype=np.uint64)
+    opp = np.zeros((E, W), dtype=np.uint64)
+    for a in range(n * n):
+        mover[:, a // 64] |= (cells[:, a] == 1).astype(np.uint64) << np.uint64(a % 64)
+        opp[:, a // 64] |= (cells[:, a] == 2).astype(np.uint64) << np.uint64(a % 64)
+    out = legal_moves(n, t64(torch, mover), t64(torch, opp))
+    np.testing.assert_array_equal(np_u64(out), oracle.legal(n, mover, opp))
+
+
+def test_sharding_is_invisible(torch_cuda):
+    """Two shards (env_id_base 0 and E/2) reproduce one unsharded handle."""
+    torch = torch_cuda
+    E = 8192
+    whole = make_env(torch, E, 8, auto=True, seed=21)
+    lo = make_env(torch, E // 2, 8, auto=True, seed=21, id_base=0)
+    hi = make_env(torch, E // 2, 8, auto=True, seed=21, id_base=E // 2)
+    aw, _, _ = whole.step_policy("random", n_plies=150)
+    al, _, _ = lo.step_policy("random", n_plies=150)
+    ah, _, _ = hi.step_policy("random", n_plies=150)
+    assert torch.equal(aw, torch.cat([al, ah], dim=1))
+    assert torch.equal(whole.counts(), lo.counts() + hi.counts())
+
+
+def test_full_size_invariants(torch_cuda):
+    """1,048,576 boards (config 4's global size on one GPU), 400 plies: structural
+    invariants that need no oracle -- colours disjoint, legal squares empty,
+    finished games == tally, every board finished >= 5 games."""
+    torch = torch_cuda
+    E = 1 << 20
+    env = make_env(torch, E, 8, auto=True, seed=99)
+    _, _, dones = env.step_policy("random", n_plies=400, record=True)
+    b, m, lg = env.get_state()
+    assert int((b[:, 0] & b[:, 1]).count_nonzero()) == 0
+    assert int((lg[:, 0] & (b[:, 0] | b[:, 1])).count_nonzero()) == 0
+    wdl = env.counts()
+    assert int(wdl.sum()) == int(dones.sum())
+    assert int(dones.sum(0).min()) >= 5
+    frac = (wdl.double() / wdl.sum()).cpu().numpy()
+    assert 0.43 < frac[0] < 0.49 and 0.03 < frac[1] < 0.06 and 0.47 < frac[2] < 0.53
+
+
+def test_state_dict_roundtrip(torch_cuda):
+    torch = torch_cuda
+    a = make_env(torch, 1000, 8, auto=True, seed=4)
+    a.step_policy("random", n_plies=33)
+    sd = a.state_dict()
+    b = make_env(torch, 1000, 8, auto=True, seed=4)
+    b.load_state_dict(sd)
+    x, _, _ = a.step_policy("random", n_plies=50)
+    y, _, _ = b.step_policy("random", n_plies=50)
+    assert torch.equal(x, y)
