@@ -81,8 +81,19 @@ def load(require_gpu=True):
     return _lib
 
 
-def check(rc, what=""):
+def load_path(path):
+    """Load another build of the same C ABI (A/B experiments: tools/ab_variants.py)."""
+    import torch  # noqa: F401
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+def check(rc, what="", lib=None):
     if rc != OTH_OK:
-        msg = _lib.oth_last_error().decode() if _lib is not None else ""
+        msg = (lib or _lib).oth_last_error().decode() if (lib or _lib) is not None else ""
         raise OthelloLibError("%s failed (%d): %s" % (what or "oth call", rc, msg))
     return rc

@@ -118,9 +118,67 @@ OTH_HD int popcount(const BB<W>& a) {
     return c;
 }
 
+#ifndef OTH_SHIFT32
+#define OTH_SHIFT32 0
+#endif
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// ({hi, lo} >> c)[31:0]: one full-rate VALU op (v_alignbit_b32)
+__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t c) {
+    return __builtin_amdgcn_alignbit(hi, lo, c);
+}
+#endif
+
 // Logical shift of the whole W-word board by S bits (S > 0 toward higher squares).
 template <int W, int S>
 OTH_HD BB<W> shift(const BB<W>& x) {
+#if defined(__HIP_DEVICE_COMPILE__) && OTH_SHIFT32
+    // On the device the board is handled as 2W dwords: each output dword is one
+    // funnel shift of two input dwords (v_alignbit_b32), instead of 64-bit
+    // shifts (v_lshlrev_b64 / v_lshrrev_b64) plus or-combines.
+    if constexpr (S != 0) {
+        constexpr int D = 2 * W;
+        uint32_t v[D], r[D];
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+            v[2 * i] = (uint32_t)x.w[i];
+            v[2 * i + 1] = (uint32_t)(x.w[i] >> 32);
+        }
+        if constexpr (S > 0) {
+            constexpr int q = S / 32, s = S % 32;
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                if (i - q < 0) {
+                    r[i] = 0;
+                } else if (s == 0) {
+                    r[i] = v[i - q];
+                } else if (i - q - 1 < 0) {
+                    r[i] = v[i - q] << s;
+                } else {
+                    r[i] = funnel(v[i - q], v[i - q - 1], 32 - s);
+                }
+            }
+        } else {
+            constexpr int T = -S, q = T / 32, s = T % 32;
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                if (i + q >= D) {
+                    r[i] = 0;
+                } else if (s == 0) {
+                    r[i] = v[i + q];
+                } else if (i + q + 1 >= D) {
+                    r[i] = v[i + q] >> s;
+                } else {
+                    r[i] = funnel(v[i + q + 1], v[i + q], s);
+                }
+            }
+        }
+        BB<W> out;
+#pragma unroll
+        for (int i = 0; i < W; ++i) out.w[i] = ((uint64_t)r[2 * i + 1] << 32) | r[2 * i];
+        return out;
+    }
+#endif
     if constexpr (S == 0) {
         return x;
     } else if constexpr (S > 0) {
@@ -175,42 +233,68 @@ struct Geo {
     }
 };
 
-template <int N, int DR, int DC>
-OTH_HD BB<Geo<N>::W> step_dir(const BB<Geo<N>::W>& x) {
-    constexpr int W = Geo<N>::W;
-    return shift<W, DR * N + DC>(x) & Geo<N>::template dst_mask<DC>();
+#ifndef OTH_ANDOR
+#define OTH_ANDOR 0
+#endif
+
+// (a & b) | c.  hipcc does not fuse 64-bit and/or pairs into v_and_or_b32
+// (it does for 32-bit values), so on the device each 32-bit half is one
+// explicit v_and_or_b32: 2 VALU ops per word instead of 4.
+template <int W>
+OTH_HD BB<W> and_or(const BB<W>& a, const BB<W>& b, const BB<W>& c) {
+#if defined(__HIP_DEVICE_COMPILE__) && OTH_ANDOR
+    BB<W> r;
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+        uint32_t lo, hi;
+        asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(lo) : "v"((uint32_t)a.w[i]), "v"((uint32_t)b.w[i]),
+            "v"((uint32_t)c.w[i]));
+        asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(hi) : "v"((uint32_t)(a.w[i] >> 32)),
+            "v"((uint32_t)(b.w[i] >> 32)), "v"((uint32_t)(c.w[i] >> 32)));
+        r.w[i] = ((uint64_t)hi << 32) | lo;
+    }
+    return r;
+#else
+    return (a & b) | c;
+#endif
 }
 
-// Extend `t` (a set of opponent squares adjacent, in direction D, to the
-// generator) through the contiguous opponent discs O along D: Kogge-Stone
-// doubling over propagator pro = O & dst_mask, enough steps for run N-2.
+// Propagators of one direction for the discs O: pro[k] holds the squares x with
+// x, x-S, ..., x-(2^k - 1)S all in O & dst_mask (Kogge-Stone doubling).  They
+// depend only on O, so one set serves every ray cast through O in that direction.
 template <int N, int DR, int DC>
-OTH_HD BB<Geo<N>::W> run_fill(BB<Geo<N>::W> t, const BB<Geo<N>::W>& O) {
-    constexpr int W = Geo<N>::W;
-    constexpr int S = DR * N + DC;
-    BB<W> pro = O & Geo<N>::template dst_mask<DC>();
-    t |= pro & shift<W, S>(t);  // runs of length <= 2
-    if constexpr (Geo<N>::MAXRUN > 2) {
-        pro &= shift<W, S>(pro);
-        t |= pro & shift<W, 2 * S>(t);  // <= 4
+struct Pro {
+    static constexpr int W = Geo<N>::W;
+    static constexpr int S = DR * N + DC;
+    static constexpr int STEPS = Geo<N>::MAXRUN > 8 ? 4 : (Geo<N>::MAXRUN > 4 ? 3 : (Geo<N>::MAXRUN > 2 ? 2 : 1));
+    BB<W> p1, p2, p4, p8;
+    OTH_HD explicit Pro(const BB<W>& O) {
+        p1 = O & Geo<N>::template dst_mask<DC>();
+        if constexpr (STEPS > 1) p2 = p1 & shift<W, S>(p1);
+        if constexpr (STEPS > 2) p4 = p2 & shift<W, 2 * S>(p2);
+        if constexpr (STEPS > 3) p8 = p4 & shift<W, 4 * S>(p4);
     }
-    if constexpr (Geo<N>::MAXRUN > 4) {
-        pro &= shift<W, 2 * S>(pro);
-        t |= pro & shift<W, 4 * S>(t);  // <= 8
+    // Extend `t` (opponent squares next to the generator) through the
+    // contiguous opponent run along the direction: runs up to 2^STEPS long.
+    OTH_HD BB<W> fill(BB<W> t) const {
+        t = and_or(p1, shift<W, S>(t), t);
+        if constexpr (STEPS > 1) t = and_or(p2, shift<W, 2 * S>(t), t);
+        if constexpr (STEPS > 2) t = and_or(p4, shift<W, 4 * S>(t), t);
+        if constexpr (STEPS > 3) t = and_or(p8, shift<W, 8 * S>(t), t);
+        return t;
     }
-    if constexpr (Geo<N>::MAXRUN > 8) {
-        pro &= shift<W, 4 * S>(pro);
-        t |= pro & shift<W, 8 * S>(t);  // <= 16
-    }
-    return t;
-}
+    // squares of the run starting one step from the generator g
+    OTH_HD BB<W> run_from(const BB<W>& g) const { return fill(shift<W, S>(g) & p1); }
+};
 
-// Legal squares for the side owning P against O, along one direction.
+// Legal squares for the mover P along one direction, or-ed into L (unmasked
+// by emptiness; legal_moves applies that once).
 template <int N, int DR, int DC>
-OTH_HD BB<Geo<N>::W> legal_dir(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O) {
-    auto t = step_dir<N, DR, DC>(P) & O;
-    t = run_fill<N, DR, DC>(t, O);
-    return step_dir<N, DR, DC>(t);
+OTH_HD void legal_dir(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O, BB<Geo<N>::W>& L) {
+    constexpr int W = Geo<N>::W;
+    const Pro<N, DR, DC> pro(O);
+    const BB<W> t = pro.run_from(P);
+    L = and_or(shift<W, DR * N + DC>(t), Geo<N>::template dst_mask<DC>(), L);
 }
 
 // get_possible_actions (othello.py:313-343) as a mask: empty squares from
@@ -219,36 +303,41 @@ OTH_HD BB<Geo<N>::W> legal_dir(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O) {
 // pairs it accepts is the same as the reference's per-cell scan.
 template <int N>
 OTH_HD BB<Geo<N>::W> legal_moves(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O) {
-    auto L = legal_dir<N, 0, 1>(P, O);
-    L |= legal_dir<N, 0, -1>(P, O);
-    L |= legal_dir<N, 1, 0>(P, O);
-    L |= legal_dir<N, -1, 0>(P, O);
-    L |= legal_dir<N, 1, 1>(P, O);
-    L |= legal_dir<N, 1, -1>(P, O);
-    L |= legal_dir<N, -1, 1>(P, O);
-    L |= legal_dir<N, -1, -1>(P, O);
+    auto L = zero<Geo<N>::W>();
+    legal_dir<N, 0, 1>(P, O, L);
+    legal_dir<N, 0, -1>(P, O, L);
+    legal_dir<N, 1, 0>(P, O, L);
+    legal_dir<N, -1, 0>(P, O, L);
+    legal_dir<N, 1, 1>(P, O, L);
+    legal_dir<N, 1, -1>(P, O, L);
+    legal_dir<N, -1, 1>(P, O, L);
+    legal_dir<N, -1, -1>(P, O, L);
     return L & ~(P | O) & Geo<N>::BOARD;
 }
 
 template <int N, int DR, int DC>
-OTH_HD BB<Geo<N>::W> flips_dir(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O, const BB<Geo<N>::W>& m) {
-    auto t = step_dir<N, DR, DC>(m) & O;
-    t = run_fill<N, DR, DC>(t, O);
-    return select_if(any(step_dir<N, DR, DC>(t) & P), t);
+OTH_HD void flips_dir(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O, const BB<Geo<N>::W>& m,
+                      BB<Geo<N>::W>& f) {
+    constexpr int W = Geo<N>::W;
+    const Pro<N, DR, DC> pro(O);
+    const BB<W> t = pro.run_from(m);
+    const bool capped = any(shift<W, DR * N + DC>(t) & (P & Geo<N>::template dst_mask<DC>()));
+    f = and_or(t, select_if(capped, ~zero<W>()), f);
 }
 
 // update_board's flips (othello.py:391-410): for each direction, the run of
 // opponent discs starting next to the move, kept only if capped by an own disc.
 template <int N>
 OTH_HD BB<Geo<N>::W> flips(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O, const BB<Geo<N>::W>& m) {
-    auto f = flips_dir<N, 0, 1>(P, O, m);
-    f |= flips_dir<N, 0, -1>(P, O, m);
-    f |= flips_dir<N, 1, 0>(P, O, m);
-    f |= flips_dir<N, -1, 0>(P, O, m);
-    f |= flips_dir<N, 1, 1>(P, O, m);
-    f |= flips_dir<N, 1, -1>(P, O, m);
-    f |= flips_dir<N, -1, 1>(P, O, m);
-    f |= flips_dir<N, -1, -1>(P, O, m);
+    auto f = zero<Geo<N>::W>();
+    flips_dir<N, 0, 1>(P, O, m, f);
+    flips_dir<N, 0, -1>(P, O, m, f);
+    flips_dir<N, 1, 0>(P, O, m, f);
+    flips_dir<N, -1, 0>(P, O, m, f);
+    flips_dir<N, 1, 1>(P, O, m, f);
+    flips_dir<N, 1, -1>(P, O, m, f);
+    flips_dir<N, -1, 1>(P, O, m, f);
+    flips_dir<N, -1, -1>(P, O, m, f);
     return f;
 }
 
@@ -297,9 +386,12 @@ OTH_HD int select_bit(const BB<W>& b, int k) {
 // Philox4x32-10 (Salmon et al., SC'11): the env RNG.  Counter = {env id,
 // ply lo, ply hi, purpose}, key = seed.  Stateless, so results do not depend on
 // how envs are sharded over GPUs or batched over launches.
-OTH_HD uint32_t philox_x(uint64_t seed, uint32_t id, uint64_t ply, uint32_t purpose) {
+struct U4 {
+    uint32_t x, y, z, w;
+};
+OTH_HD U4 philox4(uint64_t seed, uint32_t id, uint64_t ctr, uint32_t purpose) {
     uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-    uint32_t c0 = id, c1 = (uint32_t)ply, c2 = (uint32_t)(ply >> 32), c3 = purpose;
+    uint32_t c0 = id, c1 = (uint32_t)ctr, c2 = (uint32_t)(ctr >> 32), c3 = purpose;
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
         uint64_t p0 = (uint64_t)0xD2511F53u * c0;
@@ -315,7 +407,16 @@ OTH_HD uint32_t philox_x(uint64_t seed, uint32_t id, uint64_t ply, uint32_t purp
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
     }
-    return c0;
+    return U4{c0, c1, c2, c3};
+}
+OTH_HD uint32_t philox_x(uint64_t seed, uint32_t id, uint64_t ply, uint32_t purpose) {
+    return philox4(seed, id, ply, purpose).x;
+}
+OTH_HD uint32_t pick4(const U4& u, uint32_t j) { return j == 0 ? u.x : (j == 1 ? u.y : (j == 2 ? u.z : u.w)); }
+// The random-move draw of ply g: word g % 4 of the block counter g / 4, so one
+// Philox evaluation serves four consecutive plies of a board.
+OTH_HD uint32_t action_draw(uint64_t seed, uint32_t id, uint64_t g) {
+    return pick4(philox4(seed, id, g >> 2, 0), (uint32_t)(g & 3));
 }
 
 // floor(u * n / 2^32): uniform index in [0, n) (RandomPolicy, simple_policies.py:39).

@@ -25,9 +25,16 @@
 
 using namespace oth;
 
+#ifndef OTH_PAIR
+#define OTH_PAIR 0  // 1: two lanes per board for N <= 8 in k_play (measured slower)
+#endif
+#ifndef OTH_BLOCK
+#define OTH_BLOCK 256
+#endif
+
 namespace {
 
-constexpr int BLOCK = 256;
+constexpr int BLOCK = OTH_BLOCK;
 constexpr uint32_t M_TURN_WHITE = 1u;
 constexpr uint32_t M_TERMINATED = 2u;
 constexpr int M_WINNER_SHIFT = 2;
@@ -103,6 +110,105 @@ __device__ __forceinline__ void store_lane(const Lane<N>& s, uint64_t* __restric
     meta[e] = (uint16_t)s.meta;
 }
 
+// ---------------------------------------------------------------------------
+// Engines: who computes legal moves and flips for a lane.
+//   Solo<N>: one lane per board, all 8 directions (any N).
+//   Pair<N>: two lanes per board (N <= 8, one word): each lane of the pair
+//            scans 4 of the 8 directions and the halves are or-ed through a DPP
+//            quad_perm swap.  Twice the waves for the same boards, so two waves
+//            share each SIMD's issue slots instead of one wave issuing alone.
+// ---------------------------------------------------------------------------
+template <int N>
+struct Solo {
+    static constexpr int LANES = 1;
+    __device__ __forceinline__ explicit Solo(int) {}
+    __device__ __forceinline__ BB<Geo<N>::W> legal(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O) const {
+        return legal_moves<N>(P, O);
+    }
+    __device__ __forceinline__ BB<Geo<N>::W> flip(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O,
+                                                  const BB<Geo<N>::W>& m) const {
+        return flips<N>(P, O, m);
+    }
+    __device__ __forceinline__ bool leader() const { return true; }
+};
+
+// the other lane of the pair (lanes 2k, 2k+1): DPP quad_perm [1,0,3,2]
+__device__ __forceinline__ uint32_t pair_swap32(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint64_t pair_swap(uint64_t x) {
+    return ((uint64_t)pair_swap32((uint32_t)(x >> 32)) << 32) | pair_swap32((uint32_t)x);
+}
+
+template <int N>
+struct Pair {
+    static_assert(Geo<N>::W == 1, "Pair engine is for one-word boards (N <= 8)");
+    static constexpr int LANES = 2;
+    static constexpr int STEPS = Pro<N, 0, 1>::STEPS;
+    static constexpr uint64_t NC0 = Geo<N>::NOT_COL0.w[0], NCN = Geo<N>::NOT_COLN1.w[0], BD = Geo<N>::BOARD.w[0];
+    // Direction k of this lane: k even shifts toward higher squares, k odd toward lower.
+    //   lane 0: +1 (E), -1 (W), +N (S), -N (N)
+    //   lane 1: +(N+1) (SE), -(N+1) (NW), +(N-1) (SW), -(N-1) (NE)
+    // The dst masks of k = 0, 1 are the same for both lanes; k = 2, 3 are per lane.
+    uint32_t sA, sB;    // shift of k = 0/1 and of k = 2/3
+    uint64_t m2, m3;    // dst masks of k = 2 and k = 3
+    int h;
+    __device__ __forceinline__ explicit Pair(int lane_half) : h(lane_half) {
+        sA = h ? N + 1 : 1;
+        sB = h ? N - 1 : N;
+        m2 = h ? NCN : BD;
+        m3 = h ? NC0 : BD;
+    }
+    template <bool UP>
+    __device__ __forceinline__ static uint64_t sh(uint64_t x, uint32_t s) {
+        return UP ? (x << s) : (x >> s);
+    }
+    // opponent run next to generator g along (shift s, mask m), Kogge-Stone
+    template <bool UP>
+    __device__ __forceinline__ static uint64_t run(uint64_t g, uint64_t O, uint32_t s, uint64_t m) {
+        const uint64_t p1 = O & m;
+        uint64_t t = sh<UP>(g, s) & p1;
+        t |= p1 & sh<UP>(t, s);
+        if constexpr (STEPS > 1) {
+            const uint64_t p2 = p1 & sh<UP>(p1, s);
+            t |= p2 & sh<UP>(t, 2 * s);
+            if constexpr (STEPS > 2) {
+                const uint64_t p4 = p2 & sh<UP>(p2, 2 * s);
+                t |= p4 & sh<UP>(t, 4 * s);
+            }
+        }
+        return t;
+    }
+    __device__ __forceinline__ BB<1> legal(const BB<1>& Pb, const BB<1>& Ob) const {
+        const uint64_t P = Pb.w[0], O = Ob.w[0];
+        uint64_t L = sh<true>(run<true>(P, O, sA, NC0), sA) & NC0;
+        L |= sh<false>(run<false>(P, O, sA, NCN), sA) & NCN;
+        L |= sh<true>(run<true>(P, O, sB, m2), sB) & m2;
+        L |= sh<false>(run<false>(P, O, sB, m3), sB) & m3;
+        L |= pair_swap(L);
+        BB<1> r;
+        r.w[0] = L & ~(P | O) & BD;
+        return r;
+    }
+    __device__ __forceinline__ BB<1> flip(const BB<1>& Pb, const BB<1>& Ob, const BB<1>& mb) const {
+        const uint64_t P = Pb.w[0], O = Ob.w[0], m = mb.w[0];
+        uint64_t f = 0, t;
+        t = run<true>(m, O, sA, NC0);
+        f |= (sh<true>(t, sA) & P & NC0) ? t : 0ull;
+        t = run<false>(m, O, sA, NCN);
+        f |= (sh<false>(t, sA) & P & NCN) ? t : 0ull;
+        t = run<true>(m, O, sB, m2);
+        f |= (sh<true>(t, sB) & P & m2) ? t : 0ull;
+        t = run<false>(m, O, sB, m3);
+        f |= (sh<false>(t, sB) & P & m3) ? t : 0ull;
+        f |= pair_swap(f);
+        BB<1> r;
+        r.w[0] = f;
+        return r;
+    }
+    __device__ __forceinline__ bool leader() const { return h == 0; }
+};
+
 // OthelloBaseEnv.reset (othello.py:265-271); rand_left = SimpleOthelloEnv's
 // random-opening length randint(0, k//2+1)*2 (othello.py:62-63) from Philox.
 template <int N>
@@ -118,8 +224,9 @@ __device__ __forceinline__ void reset_lane(Lane<N>& s, uint64_t seed, uint32_t i
 
 // OthelloBaseEnv.step (othello.py:412-462) for one lane.  Returns the winner
 // code (0 none) through `winner` when the game ends on this ply.
-template <int N>
-__device__ __forceinline__ void step_lane(Lane<N>& s, int a, uint32_t flags, int& reward, int& done, int& winner) {
+template <int N, typename Eng>
+__device__ __forceinline__ void step_lane(Lane<N>& s, int a, uint32_t flags, int& reward, int& done, int& winner,
+                                          const Eng& eng) {
     constexpr int W = Geo<N>::W;
     constexpr int NN = N * N;
     winner = NO_DISK;
@@ -134,7 +241,7 @@ __device__ __forceinline__ void step_lane(Lane<N>& s, int a, uint32_t flags, int
     const bool valid = a >= 0 && a < NN && test(s.legal, a);  // `action not in possible_moves` (:417)
     if (valid) {                                               // update_board (:391-410)
         const BB<W> m = square<W>(a);
-        const BB<W> f = flips<N>(P, O, m);
+        const BB<W> f = eng.flip(P, O, m);
         P |= f | m;
         O = O & ~(f | m);
     }
@@ -148,12 +255,12 @@ __device__ __forceinline__ void step_lane(Lane<N>& s, int a, uint32_t flags, int
         term = true;
         winner = sudden ? -cur : by_count;  // :475-485
     } else {               // :436-442
-        const BB<W> om = legal_moves<N>(O, P);
+        const BB<W> om = eng.legal(O, P);
         if (any(om)) {
             new_tw = !tw;
             s.legal = om;
         } else {  // opponent passes; mover again, or nobody can move
-            const BB<W> mm = legal_moves<N>(P, O);
+            const BB<W> mm = eng.legal(P, O);
             s.legal = mm;
             if (!any(mm)) {
                 term = true;
@@ -183,38 +290,57 @@ __device__ __forceinline__ void step_lane(Lane<N>& s, int a, uint32_t flags, int
     done = term ? 1 : 0;
 }
 
-// RandomPolicy.get_action (simple_policies.py:37-41): possible_moves[randint(len)].
+// RandomPolicy.get_action (simple_policies.py:37-41): possible_moves[randint(len)]
+// with u = the ply's 32-bit draw.
 template <int N>
-__device__ __forceinline__ int random_action(const Lane<N>& s, uint64_t seed, uint32_t id, uint64_t ply) {
+__device__ __forceinline__ int random_action(const Lane<N>& s, uint32_t u) {
     const int n = popcount(s.legal);
-    const int k = scale_index(philox_x(seed, id, ply, RNG_ACTION), n);
-    return select_bit(s.legal, k);
+    return select_bit(s.legal, scale_index(u, n));
 }
 
 // GreedyPolicy.get_action (simple_policies.py:69-92): the move that leaves the
 // mover the most discs = the most flips; np.argmax keeps the first (lowest
 // square) of equal counts, so scan ascending and replace only on '>'.
 template <int N>
-__device__ __forceinline__ int greedy_action(const Lane<N>& s) {
+__device__ __forceinline__ void greedy_scan(const Lane<N>& s, int parity, int stride, int& best, int& best_cnt) {
     constexpr int W = Geo<N>::W;
     const bool tw = (s.meta & M_TURN_WHITE) != 0;
     const BB<W> P = tw ? s.white : s.black;
     const BB<W> O = tw ? s.black : s.white;
-    int best = -1, best_cnt = -1;
+    best = -1;
+    best_cnt = -1;
+    int idx = 0;  // rank of the candidate among the legal moves
 #pragma unroll
     for (int i = 0; i < W; ++i) {
         uint64_t x = s.legal.w[i];
         while (x) {
             const int b = __builtin_ctzll(x);
             x &= x - 1;
-            BB<W> m = zero<W>();
-            m.w[i] = 1ull << b;
-            const int c = popcount(flips<N>(P, O, m));
-            if (c > best_cnt) {
-                best_cnt = c;
-                best = 64 * i + b;
+            if (stride == 1 || (idx & 1) == parity) {
+                BB<W> m = zero<W>();
+                m.w[i] = 1ull << b;
+                const int c = popcount(flips<N>(P, O, m));
+                if (c > best_cnt) {
+                    best_cnt = c;
+                    best = 64 * i + b;
+                }
             }
+            ++idx;
         }
+    }
+}
+
+// With a Pair engine each lane scores every other candidate (by rank), then
+// the pair keeps the larger count, the lower square on a tie.
+template <int N, typename Eng>
+__device__ __forceinline__ int greedy_action(const Lane<N>& s, const Eng& eng) {
+    int best, cnt;
+    if constexpr (Eng::LANES == 1) {
+        greedy_scan<N>(s, 0, 1, best, cnt);
+    } else {
+        greedy_scan<N>(s, eng.h, 2, best, cnt);
+        const int ob = (int)pair_swap32((uint32_t)best), oc = (int)pair_swap32((uint32_t)cnt);
+        if (oc > cnt || (oc == cnt && ob >= 0 && (best < 0 || ob < best))) best = ob;
     }
     return best;
 }
@@ -225,15 +351,79 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return v;
 }
 
+#ifndef OTH_TALLY_SLOTS
+#define OTH_TALLY_SLOTS 1
+#endif
+
+// Add this block's finished games {black wins, draws, white wins} to its own
+// slot wdl[blockIdx.x][0..2].  One slot per block: no atomics, no contention
+// (launches on a stream are ordered, and block b of every launch owns slot b);
+// oth_counts sums the slots.  Every thread of the block must call this.
 __device__ __forceinline__ void tally(unsigned long long* wdl, uint32_t b, uint32_t d, uint32_t w) {
     b = wave_sum(b);
     d = wave_sum(d);
     w = wave_sum(w);
+#if OTH_TALLY_SLOTS
+    __shared__ uint32_t part[BLOCK / 64][3];
+    const int wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        part[wave][0] = b;
+        part[wave][1] = d;
+        part[wave][2] = w;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && wdl) {
+        uint32_t sb = 0, sd = 0, sw = 0;
+#pragma unroll
+        for (int i = 0; i < BLOCK / 64; ++i) {
+            sb += part[i][0];
+            sd += part[i][1];
+            sw += part[i][2];
+        }
+        if (sb | sd | sw) {
+            unsigned long long* slot = wdl + 4 * (size_t)blockIdx.x;
+            slot[0] += sb;
+            slot[1] += sd;
+            slot[2] += sw;
+        }
+    }
+#else
     if ((threadIdx.x & 63) == 0 && wdl) {
         if (b) atomicAdd(wdl + 0, (unsigned long long)b);
         if (d) atomicAdd(wdl + 1, (unsigned long long)d);
         if (w) atomicAdd(wdl + 2, (unsigned long long)w);
     }
+#endif
+}
+
+// oth_counts: sum the per-block slots into out[3] (int64); optionally zero them.
+__global__ __launch_bounds__(256) void k_reduce_wdl(unsigned long long* __restrict__ wdl, int nslots,
+                                                   int64_t* __restrict__ out, int reset) {
+    __shared__ unsigned long long acc[256][3];
+    unsigned long long b = 0, d = 0, w = 0;
+    for (int i = threadIdx.x; i < nslots; i += 256) {
+        b += wdl[4 * (size_t)i];
+        d += wdl[4 * (size_t)i + 1];
+        w += wdl[4 * (size_t)i + 2];
+        if (reset) {
+            wdl[4 * (size_t)i] = 0;
+            wdl[4 * (size_t)i + 1] = 0;
+            wdl[4 * (size_t)i + 2] = 0;
+        }
+    }
+    acc[threadIdx.x][0] = b;
+    acc[threadIdx.x][1] = d;
+    acc[threadIdx.x][2] = w;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) {
+            acc[threadIdx.x][0] += acc[threadIdx.x + s][0];
+            acc[threadIdx.x][1] += acc[threadIdx.x + s][1];
+            acc[threadIdx.x][2] += acc[threadIdx.x + s][2];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < 3) out[threadIdx.x] = (int64_t)acc[0][threadIdx.x];
 }
 
 struct Rng {
@@ -268,7 +458,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(uint64_t* __restrict__ boards, u
         load_lane<N>(s, boards, meta, legal, e);
         const bool was_term = (s.meta & M_TERMINATED) != 0;
         int r, d, win;
-        step_lane<N>(s, actions[e], flags, r, d, win);
+        step_lane<N>(s, actions[e], flags, r, d, win, Solo<N>(0));
         if (d && !was_term) {
             cb = win == BLACK_DISK;
             cd = win == NO_DISK;
@@ -284,32 +474,41 @@ __global__ __launch_bounds__(BLOCK) void k_step(uint64_t* __restrict__ boards, u
 }
 
 // oth_step_policy: `plies` plies of on-device play with the board kept in
-// registers between plies; per-ply outputs stored [ply][E].
-template <int N, int POLICY>
+// registers between plies; per-ply outputs stored [ply][E].  Eng::LANES lanes
+// per board (Solo: 1, Pair: 2); only the pair's leader lane stores.
+template <int N, int POLICY, typename Eng>
 __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
                                                 uint64_t* __restrict__ legal, int E, uint32_t flags, int plies,
                                                 int32_t* __restrict__ actions, int32_t* __restrict__ rewards,
                                                 uint8_t* __restrict__ dones, unsigned long long* __restrict__ wdl,
                                                 Rng rng, uint64_t ply0) {
-    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    const int gt = blockIdx.x * BLOCK + threadIdx.x;
+    const int e = gt / Eng::LANES;
+    const Eng eng(gt % Eng::LANES);
+    const bool lead = eng.leader();
     uint32_t cb = 0, cd = 0, cw = 0;
     if (e < E) {
         const uint32_t id = rng.id_base + (uint32_t)e;
         Lane<N> s;
         load_lane<N>(s, boards, meta, legal, e);
+        U4 draws{0, 0, 0, 0};
         for (int p = 0; p < plies; ++p) {
             const uint64_t g = ply0 + (uint64_t)p;
             const size_t o = (size_t)p * (size_t)E + (size_t)e;
+            // random policy: one Philox block per 4 plies (g uniform: no divergence)
+            if (POLICY == OTH_POLICY_RANDOM && (p == 0 || (g & 3) == 0)) draws = philox4(rng.seed, id, g >> 2, RNG_ACTION);
             int a = -1, r = 0, d = 1, win = NO_DISK;
             if (!(s.meta & M_TERMINATED)) {
                 const uint32_t rl = s.meta >> M_RAND_SHIFT;
                 if (POLICY == OTH_POLICY_RANDOM || rl > 0) {
-                    a = random_action<N>(s, rng.seed, id, g);
+                    const uint32_t u = POLICY == OTH_POLICY_RANDOM ? pick4(draws, (uint32_t)(g & 3))
+                                                                   : action_draw(rng.seed, id, g);
+                    a = random_action<N>(s, u);
                     if (rl > 0) s.meta -= 1u << M_RAND_SHIFT;
                 } else {
-                    a = greedy_action<N>(s);
+                    a = greedy_action<N>(s, eng);
                 }
-                step_lane<N>(s, a, flags, r, d, win);
+                step_lane<N>(s, a, flags, r, d, win, eng);
                 if (d) {
                     cb += win == BLACK_DISK;
                     cd += win == NO_DISK;
@@ -318,12 +517,15 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
                         reset_lane<N>(s, rng.seed, id, g, RNG_OPENING_AUTO, rng.init_rand);
                 }
             }
-            if (actions) actions[o] = a;
-            if (rewards) rewards[o] = r;
-            if (dones) dones[o] = (uint8_t)d;
+            if (lead) {
+                if (actions) actions[o] = a;
+                if (rewards) rewards[o] = r;
+                if (dones) dones[o] = (uint8_t)d;
+            }
         }
-        store_lane<N>(s, boards, meta, legal, e);
+        if (lead) store_lane<N>(s, boards, meta, legal, e);
     }
+    if (!lead) cb = cd = cw = 0;
     tally(wdl, cb, cd, cw);
 }
 
@@ -354,7 +556,7 @@ __global__ __launch_bounds__(BLOCK) void k_greedy(const uint64_t* __restrict__ b
     if (e >= E) return;
     Lane<N> s;
     load_lane<N>(s, boards, meta, legal, e);
-    out[e] = greedy_action<N>(s);
+    out[e] = greedy_action<N>(s, Solo<N>(0));
 }
 
 template <int N>
@@ -517,7 +719,8 @@ struct oth_env {
     uint64_t* boards;
     uint16_t* meta;
     uint64_t* legal;
-    unsigned long long* wdl;
+    unsigned long long* wdl;  // [nslots][4] per-block W/D/L slots (tally)
+    int32_t nslots;
 };
 
 namespace {
@@ -570,8 +773,10 @@ int oth_create(int32_t n_envs, int32_t board_size, uint32_t flags, uint64_t seed
     hipError_t err = hipMalloc((void**)&env->boards, E * 2 * W * sizeof(uint64_t));
     if (err == hipSuccess) err = hipMalloc((void**)&env->meta, ((E * sizeof(uint16_t) + 15) / 16) * 16);
     if (err == hipSuccess) err = hipMalloc((void**)&env->legal, E * W * sizeof(uint64_t));
-    if (err == hipSuccess) err = hipMalloc((void**)&env->wdl, 4 * sizeof(unsigned long long));
-    if (err == hipSuccess) err = hipMemset(env->wdl, 0, 4 * sizeof(unsigned long long));
+    env->nslots = (int32_t)((2 * E + BLOCK - 1) / BLOCK);  // the widest grid (Pair: 2 lanes per board)
+    const size_t slot_bytes = (size_t)env->nslots * 4 * sizeof(unsigned long long);
+    if (err == hipSuccess) err = hipMalloc((void**)&env->wdl, slot_bytes);
+    if (err == hipSuccess) err = hipMemset(env->wdl, 0, slot_bytes);
     if (err != hipSuccess) {
         oth_destroy(env);
         return hip_fail(err, "oth_create: allocation");
@@ -633,14 +838,28 @@ int oth_step_policy(oth_env* env, int32_t policy, int32_t n_plies, int32_t* acti
     env->ply += (uint64_t)n_plies;
     return with_n(env->n, [&](auto NC) {
         constexpr int N = decltype(NC)::value;
-        if (policy == OTH_POLICY_RANDOM)
-            hipLaunchKernelGGL((k_play<N, OTH_POLICY_RANDOM>), dim3(grid_for(env->E)), dim3(BLOCK), 0,
-                               (hipStream_t)stream, env->boards, env->meta, env->legal, env->E, env->flags, n_plies,
-                               actions, rewards, dones, env->wdl, rng_of(env), ply0);
-        else
-            hipLaunchKernelGGL((k_play<N, OTH_POLICY_GREEDY>), dim3(grid_for(env->E)), dim3(BLOCK), 0,
-                               (hipStream_t)stream, env->boards, env->meta, env->legal, env->E, env->flags, n_plies,
-                               actions, rewards, dones, env->wdl, rng_of(env), ply0);
+        hipStream_t st = (hipStream_t)stream;
+        if constexpr (Geo<N>::W == 1 && OTH_PAIR) {
+            const dim3 grid(grid_for(2ll * env->E));
+            if (policy == OTH_POLICY_RANDOM)
+                hipLaunchKernelGGL((k_play<N, OTH_POLICY_RANDOM, Pair<N>>), grid, dim3(BLOCK), 0, st, env->boards,
+                                   env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards, dones,
+                                   env->wdl, rng_of(env), ply0);
+            else
+                hipLaunchKernelGGL((k_play<N, OTH_POLICY_GREEDY, Pair<N>>), grid, dim3(BLOCK), 0, st, env->boards,
+                                   env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards, dones,
+                                   env->wdl, rng_of(env), ply0);
+        } else {
+            const dim3 grid(grid_for(env->E));
+            if (policy == OTH_POLICY_RANDOM)
+                hipLaunchKernelGGL((k_play<N, OTH_POLICY_RANDOM, Solo<N>>), grid, dim3(BLOCK), 0, st, env->boards,
+                                   env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards, dones,
+                                   env->wdl, rng_of(env), ply0);
+            else
+                hipLaunchKernelGGL((k_play<N, OTH_POLICY_GREEDY, Solo<N>>), grid, dim3(BLOCK), 0, st, env->boards,
+                                   env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards, dones,
+                                   env->wdl, rng_of(env), ply0);
+        }
         return after_launch("oth_step_policy");
     });
 }
@@ -741,9 +960,14 @@ int oth_counts(oth_env* env, int64_t* out, int32_t reset, oth_stream_t stream) {
     OTH_CHECK_ENV(env);
     if (!out) return fail(OTH_EINVAL, "out is NULL");
     hipStream_t s = (hipStream_t)stream;
+#if OTH_TALLY_SLOTS
+    hipLaunchKernelGGL(k_reduce_wdl, dim3(1), dim3(256), 0, s, env->wdl, env->nslots, out, reset ? 1 : 0);
+    return after_launch("oth_counts");
+#else
     OTH_HIP(hipMemcpyAsync(out, env->wdl, 3 * sizeof(int64_t), hipMemcpyDefault, s));
     if (reset) OTH_HIP(hipMemsetAsync(env->wdl, 0, 4 * sizeof(unsigned long long), s));
     return OTH_OK;
+#endif
 }
 
 uint64_t oth_ply_counter(const oth_env* env) { return env ? env->ply : 0; }

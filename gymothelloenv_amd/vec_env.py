@@ -42,8 +42,8 @@ class VecOthelloEnv(object):
 
     def __init__(self, num_envs, board_size=8, sudden_death_on_invalid_move=True,
                  num_disk_as_reward=False, possible_actions_in_obs=False, auto_reset=False,
-                 initial_rand_steps=0, seed=0, env_id_base=0, device=None):
-        self._lib = L.load()
+                 initial_rand_steps=0, seed=0, env_id_base=0, device=None, lib=None):
+        self._lib = lib if lib is not None else L.load()
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = torch.device(device)

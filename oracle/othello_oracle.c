@@ -347,9 +347,12 @@ int oracle_step_batch(int n, uint32_t flags, uint64_t seed, uint32_t id_base, ui
 }
 
 /* RandomPolicy.get_action (simple_policies.py:37-41) with the device RNG:
- * index k = floor(u32 * len / 2^32) into the ascending possible_moves list. */
+ * index k = floor(u32 * len / 2^32) into the ascending possible_moves list;
+ * u = word (ply % 4) of the Philox block with counter ply / 4. */
 static int random_action(const oenv *e, uint64_t seed, uint32_t id, uint64_t ply) {
-    uint32_t u = draw(seed, id, ply, 0);
+    uint32_t c[4] = {id, (uint32_t)(ply >> 2), (uint32_t)(ply >> 34), 0};
+    philox((uint32_t)seed, (uint32_t)(seed >> 32), c);
+    uint32_t u = c[ply & 3];
     int k = (int)(((uint64_t)u * (uint64_t)e->nmoves) >> 32);
     return e->moves[k];
 }
