@@ -29,6 +29,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+METRIC = "env-steps/sec (random policy, 65,536\u00d78\u00d78 boards) at 1/2/4/8 GPUs; HBM GB/s vs peak"
 
 
 def algorithmic_bytes_per_launch(E, W, plies, record=True):
@@ -63,14 +64,18 @@ def cpu_baseline(seconds, board_size=8):
                       % (E, plies, steps, board_size, board_size, dt)}
 
 
-def load_traffic(workload):
+# VALU issue peak: 256 CUs x 4 SIMD32 x one wave64 instruction per 2 cycles at 2.4 GHz
+VALU_PEAK_WAVE_INSTS = 256 * 4 * 2.4e9 / 2
+
+
+def load_pmc(workload):
+    """The rocprofv3 PMC summary of this workload committed under profiles/
+    (tools/pmc_profile.sh + tools/pmc_summarize.py), or None."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
         return None
     try:
-        d = json.load(open(p))
-        rec = d.get(workload)
-        return None if rec is None else rec["hbm_bytes_per_launch"]
+        return json.load(open(p)).get(workload)
     except Exception:
         return None
 
@@ -105,7 +110,7 @@ def main():
 
     E, n = args.envs, args.board_size
     W = nwords(n)
-    P = args.plies_per_launch or (50 if args.policy == "random" else 10)
+    P = args.plies_per_launch or (100 if args.policy == "random" else 10)
     steps = max(P, (args.steps // P) * P)
     warm = max(P, (args.warmup // P) * P) if args.warmup > 0 else 0
     launches = steps // P
@@ -159,9 +164,11 @@ def main():
         achieved = bytes_launch / avg_launch_s / 1e9
         workload = "random-play-%dx%d-E%d-P%d" % (n, n, E, P) if args.policy == "random" else \
             "greedy-play-%dx%d-E%d-P%d" % (n, n, E, P)
+        if not record:
+            workload += "-norecord"
+        pmc = load_pmc(workload)
         out = {
-            "metric": "env-steps/sec (random policy, 65,536x8x8 boards per GPU)" if args.policy == "random"
-            else "env-steps/sec (greedy policy)",
+            "metric": METRIC if args.policy == "random" else "env-steps/sec (greedy policy, on-device argmax flips)",
             "value": value,
             "unit": "env-steps/s",
             "n_gpus": world,
@@ -177,9 +184,16 @@ def main():
                        "global_boards": E * world, "plies_per_launch": P, "policy": args.policy,
                        "per_ply_outputs_stored": record, "parallelism": "dp%d (independent shards)" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBPS, "traffic": load_traffic(workload),
+                         "frac": achieved / HBM_PEAK_GBPS,
+                         "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
                          "kernel": "k_play<%d,%s>" % (n, args.policy), "avg_launch_us": avg_launch_s * 1e6,
-                         "algorithmic_bytes_per_launch": bytes_launch},
+                         "algorithmic_bytes_per_launch": bytes_launch,
+                         "valu": None if not pmc or not pmc.get("valu_insts_per_launch") else {
+                             "achieved_wave_insts_per_s": pmc["valu_insts_per_launch"] / avg_launch_s,
+                             "peak_wave_insts_per_s": VALU_PEAK_WAVE_INSTS,
+                             "frac": pmc["valu_insts_per_launch"] / avg_launch_s / VALU_PEAK_WAVE_INSTS,
+                             "note": "the kernel's real limiter: integer VALU issue (one wave per SIMD at "
+                                     "65,536 boards), see DESIGN.md"}},
             "wdl": {"black_wins": wdl_total[0], "draws": wdl_total[1], "white_wins": wdl_total[2]},
         }
         if not args.no_cpu_baseline and world == 1:

@@ -28,6 +28,9 @@ using namespace oth;
 #ifndef OTH_PAIR
 #define OTH_PAIR 0  // 1: two lanes per board for N <= 8 in k_play (measured slower)
 #endif
+#ifndef OTH_RAYS
+#define OTH_RAYS 1  // LDS ray-table flips for N <= 8 in k_play
+#endif
 #ifndef OTH_BLOCK
 #define OTH_BLOCK 256
 #endif
@@ -121,13 +124,76 @@ __device__ __forceinline__ void store_lane(const Lane<N>& s, uint64_t* __restric
 template <int N>
 struct Solo {
     static constexpr int LANES = 1;
-    __device__ __forceinline__ explicit Solo(int) {}
+    static constexpr int RAY_WORDS = 0;
+    __device__ __forceinline__ Solo(int, const uint64_t*) {}
     __device__ __forceinline__ BB<Geo<N>::W> legal(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O) const {
         return legal_moves<N>(P, O);
     }
-    __device__ __forceinline__ BB<Geo<N>::W> flip(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O,
-                                                  const BB<Geo<N>::W>& m) const {
-        return flips<N>(P, O, m);
+    __device__ __forceinline__ BB<Geo<N>::W> flip(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O, int a) const {
+        return flips<N>(P, O, square<Geo<N>::W>(a));
+    }
+    __device__ __forceinline__ bool leader() const { return true; }
+};
+
+// Ray tables for one-word boards: rays[d*64 + sq] = the squares strictly beyond
+// sq in direction d, up to the edge.  d 0..3 point to higher squares (E, S, SE,
+// SW), d 4..7 to lower ones (W, N, NW, NE).  Built in LDS once per launch.
+__device__ __constant__ const int RAY_DR[8] = {0, 1, 1, 1, 0, -1, -1, -1};
+__device__ __constant__ const int RAY_DC[8] = {1, 0, 1, -1, -1, 0, -1, 1};
+
+template <int N>
+__device__ __forceinline__ void fill_rays(uint64_t* rays) {
+    for (int i = threadIdx.x; i < 8 * 64; i += BLOCK) {
+        const int d = i >> 6, sq = i & 63;
+        uint64_t r = 0;
+        if (sq < N * N) {
+            const int dr = RAY_DR[d], dc = RAY_DC[d];
+            int row = sq / N + dr, col = sq % N + dc;
+            while (row >= 0 && row < N && col >= 0 && col < N) {
+                r |= 1ull << (row * N + col);
+                row += dr;
+                col += dc;
+            }
+        }
+        rays[i] = r;
+    }
+    __syncthreads();
+}
+
+// update_board's flips from one square (othello.py:391-410) with the ray
+// tables: along each ray the run is capped by the NEAREST non-opponent square
+// (lowest set bit of ray & ~O toward higher squares, highest toward lower);
+// the run flips iff that square holds an own disc.  ~20 VALU per direction
+// against ~33 for a Kogge-Stone fill from a single square.
+template <int N>
+struct Rays {
+    static_assert(Geo<N>::W == 1, "ray tables are for one-word boards (N <= 8)");
+    static constexpr int LANES = 1;
+    static constexpr int RAY_WORDS = 8 * 64;
+    const uint64_t* rays;
+    __device__ __forceinline__ Rays(int, const uint64_t* lds) : rays(lds) {}
+    __device__ __forceinline__ BB<1> legal(const BB<1>& P, const BB<1>& O) const { return legal_moves<N>(P, O); }
+    __device__ __forceinline__ BB<1> flip(const BB<1>& Pb, const BB<1>& Ob, int a) const {
+        const uint64_t P = Pb.w[0], nO = ~Ob.w[0];
+        const uint64_t* r = rays + a;
+        uint64_t f = 0;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {  // toward higher squares
+            const uint64_t ray = r[64 * d];
+            const uint64_t x = ray & nO;
+            const uint64_t fb = x & (0ull - x);
+            f |= (fb & P) ? (ray & (fb - 1ull)) : 0ull;
+        }
+#pragma unroll
+        for (int d = 4; d < 8; ++d) {  // toward lower squares
+            const uint64_t ray = r[64 * d];
+            const uint64_t x = ray & nO;
+            const uint64_t hb = x ? (0x8000000000000000ull >> __clzll(x)) : 0ull;
+            f |= (hb & P) ? (ray & (0ull - (hb << 1))) : 0ull;
+        }
+        BB<1> out;
+        out.w[0] = f;
+        return out;
     }
     __device__ __forceinline__ bool leader() const { return true; }
 };
@@ -153,7 +219,8 @@ struct Pair {
     uint32_t sA, sB;    // shift of k = 0/1 and of k = 2/3
     uint64_t m2, m3;    // dst masks of k = 2 and k = 3
     int h;
-    __device__ __forceinline__ explicit Pair(int lane_half) : h(lane_half) {
+    static constexpr int RAY_WORDS = 0;
+    __device__ __forceinline__ Pair(int lane_half, const uint64_t*) : h(lane_half) {
         sA = h ? N + 1 : 1;
         sB = h ? N - 1 : N;
         m2 = h ? NCN : BD;
@@ -190,8 +257,8 @@ struct Pair {
         r.w[0] = L & ~(P | O) & BD;
         return r;
     }
-    __device__ __forceinline__ BB<1> flip(const BB<1>& Pb, const BB<1>& Ob, const BB<1>& mb) const {
-        const uint64_t P = Pb.w[0], O = Ob.w[0], m = mb.w[0];
+    __device__ __forceinline__ BB<1> flip(const BB<1>& Pb, const BB<1>& Ob, int a) const {
+        const uint64_t P = Pb.w[0], O = Ob.w[0], m = 1ull << a;
         uint64_t f = 0, t;
         t = run<true>(m, O, sA, NC0);
         f |= (sh<true>(t, sA) & P & NC0) ? t : 0ull;
@@ -241,7 +308,7 @@ __device__ __forceinline__ void step_lane(Lane<N>& s, int a, uint32_t flags, int
     const bool valid = a >= 0 && a < NN && test(s.legal, a);  // `action not in possible_moves` (:417)
     if (valid) {                                               // update_board (:391-410)
         const BB<W> m = square<W>(a);
-        const BB<W> f = eng.flip(P, O, m);
+        const BB<W> f = eng.flip(P, O, a);
         P |= f | m;
         O = O & ~(f | m);
     }
@@ -301,8 +368,9 @@ __device__ __forceinline__ int random_action(const Lane<N>& s, uint32_t u) {
 // GreedyPolicy.get_action (simple_policies.py:69-92): the move that leaves the
 // mover the most discs = the most flips; np.argmax keeps the first (lowest
 // square) of equal counts, so scan ascending and replace only on '>'.
-template <int N>
-__device__ __forceinline__ void greedy_scan(const Lane<N>& s, int parity, int stride, int& best, int& best_cnt) {
+template <int N, typename Eng>
+__device__ __forceinline__ void greedy_scan(const Lane<N>& s, int parity, int stride, int& best, int& best_cnt,
+                                            const Eng& eng) {
     constexpr int W = Geo<N>::W;
     const bool tw = (s.meta & M_TURN_WHITE) != 0;
     const BB<W> P = tw ? s.white : s.black;
@@ -317,9 +385,14 @@ __device__ __forceinline__ void greedy_scan(const Lane<N>& s, int parity, int st
             const int b = __builtin_ctzll(x);
             x &= x - 1;
             if (stride == 1 || (idx & 1) == parity) {
-                BB<W> m = zero<W>();
-                m.w[i] = 1ull << b;
-                const int c = popcount(flips<N>(P, O, m));
+                int c;
+                if constexpr (Eng::RAY_WORDS > 0) {
+                    c = popcount(eng.flip(P, O, 64 * i + b));
+                } else {
+                    BB<W> m = zero<W>();
+                    m.w[i] = 1ull << b;
+                    c = popcount(flips<N>(P, O, m));
+                }
                 if (c > best_cnt) {
                     best_cnt = c;
                     best = 64 * i + b;
@@ -336,9 +409,9 @@ template <int N, typename Eng>
 __device__ __forceinline__ int greedy_action(const Lane<N>& s, const Eng& eng) {
     int best, cnt;
     if constexpr (Eng::LANES == 1) {
-        greedy_scan<N>(s, 0, 1, best, cnt);
+        greedy_scan<N>(s, 0, 1, best, cnt, eng);
     } else {
-        greedy_scan<N>(s, eng.h, 2, best, cnt);
+        greedy_scan<N>(s, eng.h, 2, best, cnt, eng);
         const int ob = (int)pair_swap32((uint32_t)best), oc = (int)pair_swap32((uint32_t)cnt);
         if (oc > cnt || (oc == cnt && ob >= 0 && (best < 0 || ob < best))) best = ob;
     }
@@ -458,7 +531,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(uint64_t* __restrict__ boards, u
         load_lane<N>(s, boards, meta, legal, e);
         const bool was_term = (s.meta & M_TERMINATED) != 0;
         int r, d, win;
-        step_lane<N>(s, actions[e], flags, r, d, win, Solo<N>(0));
+        step_lane<N>(s, actions[e], flags, r, d, win, Solo<N>(0, nullptr));
         if (d && !was_term) {
             cb = win == BLACK_DISK;
             cd = win == NO_DISK;
@@ -482,9 +555,11 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
                                                 int32_t* __restrict__ actions, int32_t* __restrict__ rewards,
                                                 uint8_t* __restrict__ dones, unsigned long long* __restrict__ wdl,
                                                 Rng rng, uint64_t ply0) {
+    __shared__ uint64_t lds_rays[Eng::RAY_WORDS > 0 ? Eng::RAY_WORDS : 1];
+    if constexpr (Eng::RAY_WORDS > 0) fill_rays<N>(lds_rays);
     const int gt = blockIdx.x * BLOCK + threadIdx.x;
     const int e = gt / Eng::LANES;
-    const Eng eng(gt % Eng::LANES);
+    const Eng eng(gt % Eng::LANES, lds_rays);
     const bool lead = eng.leader();
     uint32_t cb = 0, cd = 0, cw = 0;
     if (e < E) {
@@ -556,7 +631,7 @@ __global__ __launch_bounds__(BLOCK) void k_greedy(const uint64_t* __restrict__ b
     if (e >= E) return;
     Lane<N> s;
     load_lane<N>(s, boards, meta, legal, e);
-    out[e] = greedy_action<N>(s, Solo<N>(0));
+    out[e] = greedy_action<N>(s, Solo<N>(0, nullptr));
 }
 
 template <int N>
@@ -847,6 +922,16 @@ int oth_step_policy(oth_env* env, int32_t policy, int32_t n_plies, int32_t* acti
                                    env->wdl, rng_of(env), ply0);
             else
                 hipLaunchKernelGGL((k_play<N, OTH_POLICY_GREEDY, Pair<N>>), grid, dim3(BLOCK), 0, st, env->boards,
+                                   env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards, dones,
+                                   env->wdl, rng_of(env), ply0);
+        } else if constexpr (Geo<N>::W == 1 && OTH_RAYS) {
+            const dim3 grid(grid_for(env->E));
+            if (policy == OTH_POLICY_RANDOM)
+                hipLaunchKernelGGL((k_play<N, OTH_POLICY_RANDOM, Rays<N>>), grid, dim3(BLOCK), 0, st, env->boards,
+                                   env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards, dones,
+                                   env->wdl, rng_of(env), ply0);
+            else
+                hipLaunchKernelGGL((k_play<N, OTH_POLICY_GREEDY, Rays<N>>), grid, dim3(BLOCK), 0, st, env->boards,
                                    env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards, dones,
                                    env->wdl, rng_of(env), ply0);
         } else {
