@@ -106,6 +106,7 @@ def main():
     dev = torch.device("cuda", local)
 
     from gymothelloenv_amd import VecOthelloEnv
+    from gymothelloenv_amd.distributed import gather_wdl, shard
     from gymothelloenv_amd.vec_env import nwords
 
     E, n = args.envs, args.board_size
@@ -115,7 +116,8 @@ def main():
     warm = max(P, (args.warmup // P) * P) if args.warmup > 0 else 0
     launches = steps // P
     record = not args.no_record
-    env = VecOthelloEnv(E, board_size=n, auto_reset=True, seed=0, env_id_base=rank * E,
+    base, _ = shard(E * world, world, rank)  # weak scaling: E boards per GPU, global ids rank*E ...
+    env = VecOthelloEnv(E, board_size=n, auto_reset=True, seed=0, env_id_base=base,
                         initial_rand_steps=10 if args.policy == "greedy" else 0, device=dev)
     env.reset()
     acts = torch.empty(P, E, dtype=torch.int32, device=dev) if record else None
@@ -148,9 +150,7 @@ def main():
     t = torch.tensor([wall], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        gathered = torch.empty(world * 3, dtype=torch.int64, device=dev)
-        dist.all_gather_into_tensor(gathered, wdl)  # RCCL over xGMI: the W/D/L tally
-        wdl_total = gathered.view(world, 3).sum(0)
+        wdl_total = gather_wdl(wdl).sum(0)  # RCCL all-gather over xGMI: the W/D/L tally
     else:
         wdl_total = wdl
     wall_max = float(t.item())

@@ -925,13 +925,15 @@ int oth_step_policy(oth_env* env, int32_t policy, int32_t n_plies, int32_t* acti
                                    env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards, dones,
                                    env->wdl, rng_of(env), ply0);
         } else if constexpr (Geo<N>::W == 1 && OTH_RAYS) {
+            // random play: ray-table flips; greedy: Kogge-Stone flips in the
+            // candidate loop (the ray tables' exposed LDS latency measured -10 %)
             const dim3 grid(grid_for(env->E));
             if (policy == OTH_POLICY_RANDOM)
                 hipLaunchKernelGGL((k_play<N, OTH_POLICY_RANDOM, Rays<N>>), grid, dim3(BLOCK), 0, st, env->boards,
                                    env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards, dones,
                                    env->wdl, rng_of(env), ply0);
             else
-                hipLaunchKernelGGL((k_play<N, OTH_POLICY_GREEDY, Rays<N>>), grid, dim3(BLOCK), 0, st, env->boards,
+                hipLaunchKernelGGL((k_play<N, OTH_POLICY_GREEDY, Solo<N>>), grid, dim3(BLOCK), 0, st, env->boards,
                                    env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards, dones,
                                    env->wdl, rng_of(env), ply0);
         } else {
