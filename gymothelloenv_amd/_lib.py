@@ -34,6 +34,8 @@ SIGNATURES = {
     "oth_reset": (_I32, [_P, _P, _P]),
     "oth_step": (_I32, [_P, _P, _P, _P, _P]),
     "oth_step_policy": (_I32, [_P, _I32, _I32, _P, _P, _P, _P]),
+    "oth_reset_vs": (_I32, [_P, _I32, _P, _P, _P]),
+    "oth_step_vs": (_I32, [_P, _I32, _P, _P, _P, _P, _P, _P]),
     "oth_legal": (_I32, [_P, _P, _P]),
     "oth_legal_moves": (_I32, [_I32, _I32, _P, _P, _P, _P]),
     "oth_greedy_actions": (_I32, [_P, _P, _P]),

@@ -224,6 +224,14 @@ struct Geo {
     static constexpr BB<W> BOARD = make_mask<-1>();
     static constexpr BB<W> NOT_COL0 = make_mask<0>();
     static constexpr BB<W> NOT_COLN1 = make_mask<N - 1>();
+    static constexpr BB<W> make_inner() {
+        BB<W> m{};
+        for (int i = 0; i < W; ++i) m.w[i] = 0;
+        for (int a = 0; a < NN; ++a)
+            if (a % N != 0 && a % N != N - 1) m.w[a / 64] |= 1ull << (a % 64);
+        return m;
+    }
+    static constexpr BB<W> INNER = make_inner();  // board minus the two edge columns
 
     // A move one step in direction (DR, DC) = shift by DR*N+DC, then drop the
     // squares that wrapped around a board edge (or fell off the last word).
@@ -297,6 +305,43 @@ OTH_HD void legal_dir(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O, BB<Geo<N>:
     L = and_or(shift<W, DR * N + DC>(t), Geo<N>::template dst_mask<DC>(), L);
 }
 
+#ifndef OTH_AXIS_LEGAL
+#define OTH_AXIS_LEGAL 1
+#endif
+
+// Both directions of one axis (shift S > 0 and -S) for the mover P against the
+// propagator p1 (opponent discs that a run may pass through).  For the
+// horizontal and diagonal axes p1 excludes the two edge columns: a run can
+// never continue through an edge-column disc along those axes, and with t kept
+// inside the inner columns no shift of t can wrap around a row, so no
+// per-shift edge masks are needed.  The -S doubling chain is the +S chain
+// shifted: p2-(y) = p2+(y+S), p4-(y) = p4+(y+3S), p8-(y) = p8+(y+7S).
+template <int N, int S>
+OTH_HD void legal_axis(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& p1, BB<Geo<N>::W>& L) {
+    constexpr int W = Geo<N>::W;
+    constexpr int STEPS = Pro<N, 0, 1>::STEPS;
+    BB<W> p2, p4, p8;
+    if constexpr (STEPS > 1) p2 = p1 & shift<W, S>(p1);
+    if constexpr (STEPS > 2) p4 = p2 & shift<W, 2 * S>(p2);
+    if constexpr (STEPS > 3) p8 = p4 & shift<W, 4 * S>(p4);
+    {  // +S
+        BB<W> t = shift<W, S>(P) & p1;
+        t |= p1 & shift<W, S>(t);
+        if constexpr (STEPS > 1) t |= p2 & shift<W, 2 * S>(t);
+        if constexpr (STEPS > 2) t |= p4 & shift<W, 4 * S>(t);
+        if constexpr (STEPS > 3) t |= p8 & shift<W, 8 * S>(t);
+        L |= shift<W, S>(t);
+    }
+    {  // -S
+        BB<W> t = shift<W, -S>(P) & p1;
+        t |= p1 & shift<W, -S>(t);
+        if constexpr (STEPS > 1) t |= shift<W, -S>(p2) & shift<W, -2 * S>(t);
+        if constexpr (STEPS > 2) t |= shift<W, -3 * S>(p4) & shift<W, -4 * S>(t);
+        if constexpr (STEPS > 3) t |= shift<W, -7 * S>(p8) & shift<W, -8 * S>(t);
+        L |= shift<W, -S>(t);
+    }
+}
+
 // get_possible_actions (othello.py:313-343) as a mask: empty squares from
 // which some direction holds >= 1 opponent disc followed by an own disc.
 // Written as rays cast FROM the mover's discs; the set of (square, direction)
@@ -304,6 +349,13 @@ OTH_HD void legal_dir(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O, BB<Geo<N>:
 template <int N>
 OTH_HD BB<Geo<N>::W> legal_moves(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O) {
     auto L = zero<Geo<N>::W>();
+#if OTH_AXIS_LEGAL
+    const auto pin = O & Geo<N>::INNER;
+    legal_axis<N, 1>(P, pin, L);      // E / W
+    legal_axis<N, N>(P, O, L);        // S / N
+    legal_axis<N, N + 1>(P, pin, L);  // SE / NW
+    legal_axis<N, N - 1>(P, pin, L);  // SW / NE
+#else
     legal_dir<N, 0, 1>(P, O, L);
     legal_dir<N, 0, -1>(P, O, L);
     legal_dir<N, 1, 0>(P, O, L);
@@ -312,6 +364,7 @@ OTH_HD BB<Geo<N>::W> legal_moves(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O)
     legal_dir<N, 1, -1>(P, O, L);
     legal_dir<N, -1, 1>(P, O, L);
     legal_dir<N, -1, -1>(P, O, L);
+#endif
     return L & ~(P | O) & Geo<N>::BOARD;
 }
 

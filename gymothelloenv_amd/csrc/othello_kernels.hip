@@ -308,7 +308,11 @@ __device__ __forceinline__ void step_lane(Lane<N>& s, int a, uint32_t flags, int
     const bool valid = a >= 0 && a < NN && test(s.legal, a);  // `action not in possible_moves` (:417)
     if (valid) {                                               // update_board (:391-410)
         const BB<W> m = square<W>(a);
+#ifdef OTH_ABLATE_NOFLIP  // timing ablation only
+        const BB<W> f = zero<W>();
+#else
         const BB<W> f = eng.flip(P, O, a);
+#endif
         P |= f | m;
         O = O & ~(f | m);
     }
@@ -323,16 +327,17 @@ __device__ __forceinline__ void step_lane(Lane<N>& s, int a, uint32_t flags, int
         winner = sudden ? -cur : by_count;  // :475-485
     } else {               // :436-442
         const BB<W> om = eng.legal(O, P);
-        if (any(om)) {
+        const bool opp_pass = !any(om);
+        BB<W> nl = om;
+#ifndef OTH_ABLATE_NOPASS
+        if (opp_pass) nl = eng.legal(P, O);
+#endif
+        s.legal = nl;
+        if (!opp_pass) {
             new_tw = !tw;
-            s.legal = om;
-        } else {  // opponent passes; mover again, or nobody can move
-            const BB<W> mm = eng.legal(P, O);
-            s.legal = mm;
-            if (!any(mm)) {
-                term = true;
-                winner = by_count;
-            }
+        } else if (!any(nl)) {  // nobody can move
+            term = true;
+            winner = by_count;
         }
     }
     if (tw) {
@@ -571,14 +576,25 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
             const uint64_t g = ply0 + (uint64_t)p;
             const size_t o = (size_t)p * (size_t)E + (size_t)e;
             // random policy: one Philox block per 4 plies (g uniform: no divergence)
+#ifdef OTH_ABLATE_RNG  // timing ablation only: a multiplicative hash instead of Philox
+            if (POLICY == OTH_POLICY_RANDOM && (p == 0 || (g & 3) == 0)) {
+                const uint32_t h = (id ^ (uint32_t)g) * 0x9E3779B9u;
+                draws = U4{h, h * 3u, h * 5u, h * 7u};
+            }
+#else
             if (POLICY == OTH_POLICY_RANDOM && (p == 0 || (g & 3) == 0)) draws = philox4(rng.seed, id, g >> 2, RNG_ACTION);
+#endif
             int a = -1, r = 0, d = 1, win = NO_DISK;
             if (!(s.meta & M_TERMINATED)) {
                 const uint32_t rl = s.meta >> M_RAND_SHIFT;
                 if (POLICY == OTH_POLICY_RANDOM || rl > 0) {
                     const uint32_t u = POLICY == OTH_POLICY_RANDOM ? pick4(draws, (uint32_t)(g & 3))
                                                                    : action_draw(rng.seed, id, g);
+#ifdef OTH_ABLATE_SELECT  // timing ablation only: lowest legal square
+                    a = __builtin_ctzll(s.legal.w[0] | (1ull << 63)) + (int)(u & 0);
+#else
                     a = random_action<N>(s, u);
+#endif
                     if (rl > 0) s.meta -= 1u << M_RAND_SHIFT;
                 } else {
                     a = greedy_action<N>(s, eng);
@@ -592,15 +608,127 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
                         reset_lane<N>(s, rng.seed, id, g, RNG_OPENING_AUTO, rng.init_rand);
                 }
             }
+#ifndef OTH_ABLATE_NOSTORE
             if (lead) {
                 if (actions) actions[o] = a;
                 if (rewards) rewards[o] = r;
                 if (dones) dones[o] = (uint8_t)d;
             }
+#endif
         }
         if (lead) store_lane<N>(s, boards, meta, legal, e);
     }
     if (!lead) cb = cd = cw = 0;
+    tally(wdl, cb, cd, cw);
+}
+
+
+// ---------------------------------------------------------------------------
+// OthelloEnv semantics on the device (othello.py:151-200): the protagonist
+// steps with the caller's action, then the embedded opponent (random or greedy,
+// on device) replies until it is the protagonist's turn again; the reward of
+// a game the opponent's ply ends is negated (:200).  Random-opening plies
+// (SimpleOthelloEnv / OthelloEnv rand_step_cnt, :179-182, :191-194) replace
+// both sides' moves by random ones; the opponent's reply inside reset() uses
+// the policy directly (:165-174).  Draws: ply j of call c uses
+// action_draw(seed, id, c * 256 + j).
+// ---------------------------------------------------------------------------
+constexpr uint64_t VS_PLIES_PER_CALL = 256;
+
+template <int N, int POLICY>
+__device__ __forceinline__ void opponent_reply(Lane<N>& s, bool prot_white, bool openings, uint32_t flags,
+                                               const Rng& rng, uint32_t id, uint64_t gbase, uint32_t& j, int& r,
+                                               int& d, int& win) {
+    const Solo<N> eng(0, nullptr);
+    while (!(s.meta & M_TERMINATED) && (((s.meta & M_TURN_WHITE) != 0) != prot_white)) {
+        const uint32_t rl = s.meta >> M_RAND_SHIFT;
+        const uint64_t g = gbase + j++;  // ply j of the call
+        int a;
+        if (POLICY == OTH_POLICY_RANDOM || (openings && rl > 0)) {
+            a = random_action<N>(s, action_draw(rng.seed, id, g));
+        } else {
+            a = greedy_action<N>(s, eng);
+        }
+        if (openings && rl > 0) s.meta -= 1u << M_RAND_SHIFT;
+        step_lane<N>(s, a, flags, r, d, win, eng);
+    }
+}
+
+template <int N, int POLICY>
+__device__ __forceinline__ void reset_vs_lane(Lane<N>& s, bool prot_white, uint32_t flags, const Rng& rng,
+                                              uint32_t id, uint64_t call, uint32_t purpose, uint32_t& j) {
+    reset_lane<N>(s, rng.seed, id, call, purpose, rng.init_rand);
+    int r, d, win;
+    opponent_reply<N, POLICY>(s, prot_white, false, flags, rng, id, call * VS_PLIES_PER_CALL, j, r, d, win);
+}
+
+template <int N, int POLICY>
+__global__ __launch_bounds__(BLOCK) void k_reset_vs(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
+                                                    uint64_t* __restrict__ legal, int E, uint32_t flags,
+                                                    const int8_t* __restrict__ prot, const uint8_t* __restrict__ mask,
+                                                    Rng rng, uint64_t call) {
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= E) return;
+    if (mask && !mask[e]) return;
+    const bool pw = prot ? prot[e] == WHITE_DISK : true;
+    Lane<N> s;
+    uint32_t j = 0;
+    reset_vs_lane<N, POLICY>(s, pw, flags, rng, rng.id_base + (uint32_t)e, call, RNG_OPENING_RESET, j);
+    store_lane<N>(s, boards, meta, legal, e);
+}
+
+template <int N, int POLICY>
+__global__ __launch_bounds__(BLOCK) void k_step_vs(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
+                                                   uint64_t* __restrict__ legal, int E, uint32_t flags,
+                                                   const int32_t* __restrict__ actions, const int8_t* __restrict__ prot,
+                                                   int32_t* __restrict__ rewards, uint8_t* __restrict__ dones,
+                                                   int32_t* __restrict__ plies_out,
+                                                   unsigned long long* __restrict__ wdl, Rng rng, uint64_t call) {
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    uint32_t cb = 0, cd = 0, cw = 0;
+    if (e < E) {
+        const uint32_t id = rng.id_base + (uint32_t)e;
+        const bool pw = prot ? prot[e] == WHITE_DISK : true;
+        const uint64_t gbase = call * VS_PLIES_PER_CALL;
+        Lane<N> s;
+        load_lane<N>(s, boards, meta, legal, e);
+        uint32_t j = 0;
+        int r = 0, d = 1, win = NO_DISK, plies = 0;
+        if (!(s.meta & M_TERMINATED)) {
+            const Solo<N> eng(0, nullptr);
+            d = 0;
+            // the protagonist must be to move (OthelloEnv.step asserts it, othello.py:177);
+            // if not, the opponent replies first, as OthelloEnv.reset does
+            opponent_reply<N, POLICY>(s, pw, true, flags, rng, id, gbase, j, r, d, win);
+            if (!(s.meta & M_TERMINATED)) {
+                int a = actions[e];
+                const uint32_t rl = s.meta >> M_RAND_SHIFT;
+                const uint64_t g = gbase + j++;
+                if (rl > 0) {  // opening ply: the protagonist's action is replaced too (:179-182)
+                    a = random_action<N>(s, action_draw(rng.seed, id, g));
+                    s.meta -= 1u << M_RAND_SHIFT;
+                }
+                step_lane<N>(s, a, flags, r, d, win, eng);
+                if (!d) {
+                    opponent_reply<N, POLICY>(s, pw, true, flags, rng, id, gbase, j, r, d, win);
+                    r = -r;  // :200
+                }
+            } else {
+                r = -r;
+            }
+            plies = (int)j;
+            if (d) {
+                cb = win == BLACK_DISK;
+                cd = win == NO_DISK;
+                cw = win == WHITE_DISK;
+                if (flags & OTH_AUTO_RESET) reset_vs_lane<N, POLICY>(s, pw, flags, rng, id, call, RNG_OPENING_AUTO, j);
+            }
+        }
+        store_lane<N>(s, boards, meta, legal, e);
+        if (rewards) rewards[e] = r;
+        if (dones) dones[e] = (uint8_t)d;
+        if (plies_out) plies_out[e] = plies;
+    }
     tally(wdl, cb, cd, cw);
 }
 
@@ -948,6 +1076,49 @@ int oth_step_policy(oth_env* env, int32_t policy, int32_t n_plies, int32_t* acti
                                    env->wdl, rng_of(env), ply0);
         }
         return after_launch("oth_step_policy");
+    });
+}
+
+int oth_reset_vs(oth_env* env, int32_t opponent_policy, const int8_t* protagonist, const uint8_t* mask,
+                 oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    if (opponent_policy != OTH_POLICY_RANDOM && opponent_policy != OTH_POLICY_GREEDY)
+        return fail(OTH_EINVAL, "unknown opponent policy");
+    const uint64_t call = env->ply++;
+    return with_n(env->n, [&](auto NC) {
+        constexpr int N = decltype(NC)::value;
+        hipStream_t st = (hipStream_t)stream;
+        if (opponent_policy == OTH_POLICY_RANDOM)
+            hipLaunchKernelGGL((k_reset_vs<N, OTH_POLICY_RANDOM>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st,
+                               env->boards, env->meta, env->legal, env->E, env->flags, protagonist, mask,
+                               rng_of(env), call);
+        else
+            hipLaunchKernelGGL((k_reset_vs<N, OTH_POLICY_GREEDY>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st,
+                               env->boards, env->meta, env->legal, env->E, env->flags, protagonist, mask,
+                               rng_of(env), call);
+        return after_launch("oth_reset_vs");
+    });
+}
+
+int oth_step_vs(oth_env* env, int32_t opponent_policy, const int32_t* actions, const int8_t* protagonist,
+                int32_t* rewards, uint8_t* dones, int32_t* plies, oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    if (!actions) return fail(OTH_EINVAL, "actions is NULL");
+    if (opponent_policy != OTH_POLICY_RANDOM && opponent_policy != OTH_POLICY_GREEDY)
+        return fail(OTH_EINVAL, "unknown opponent policy");
+    const uint64_t call = env->ply++;
+    return with_n(env->n, [&](auto NC) {
+        constexpr int N = decltype(NC)::value;
+        hipStream_t st = (hipStream_t)stream;
+        if (opponent_policy == OTH_POLICY_RANDOM)
+            hipLaunchKernelGGL((k_step_vs<N, OTH_POLICY_RANDOM>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st,
+                               env->boards, env->meta, env->legal, env->E, env->flags, actions, protagonist,
+                               rewards, dones, plies, env->wdl, rng_of(env), call);
+        else
+            hipLaunchKernelGGL((k_step_vs<N, OTH_POLICY_GREEDY>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st,
+                               env->boards, env->meta, env->legal, env->E, env->flags, actions, protagonist,
+                               rewards, dones, plies, env->wdl, rng_of(env), call);
+        return after_launch("oth_step_vs");
     });
 }
 

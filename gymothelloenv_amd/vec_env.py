@@ -134,6 +134,41 @@ class VecOthelloEnv(object):
                                           _ptr(dones), self._stream()), "oth_step_policy")
         return actions, rewards, dones
 
+    # ------------------------------------------- OthelloEnv semantics on device
+    def _protagonist(self, protagonist):
+        if protagonist is None:
+            return getattr(self, "_prot", None)
+        if isinstance(protagonist, int):
+            protagonist = torch.full((self.num_envs,), protagonist, dtype=torch.int8)
+        t = protagonist.to(device=self.device, dtype=torch.int8).contiguous()
+        if t.numel() != self.num_envs:
+            raise ValueError("protagonist needs one colour per board")
+        self._prot = t
+        return t
+
+    def reset_vs(self, opponent="random", protagonist=None, mask=None):
+        """OthelloEnv.reset (othello.py:151-174) for every board: reset, then the
+        embedded opponent (`opponent` = 'random' | 'greedy', played on the device)
+        replies until the protagonist (+1 white, the reference default, or -1
+        black; int or per-board tensor) is to move."""
+        prot = self._protagonist(protagonist)
+        m = None if mask is None else mask.to(device=self.device, dtype=torch.uint8).contiguous()
+        L.check(self._lib.oth_reset_vs(self._h, _POLICIES[opponent], _ptr(prot), _ptr(m), self._stream()),
+                "oth_reset_vs")
+        return self.get_observation()
+
+    def step_vs(self, actions, opponent="random", protagonist=None, observe=True):
+        """OthelloEnv.step (othello.py:176-200) for every board: the protagonist
+        plays `actions`, the device opponent replies until the protagonist is to
+        move again.  Returns (obs, rewards (protagonist's view, negated after an
+        opponent ply ended the game), dones bool, plies applied per board)."""
+        prot = self._protagonist(protagonist)
+        a = actions.to(device=self.device, dtype=torch.int32).contiguous()
+        r, d, n = self._i32(self.num_envs), self._u8(self.num_envs), self._i32(self.num_envs)
+        L.check(self._lib.oth_step_vs(self._h, _POLICIES[opponent], _ptr(a), _ptr(prot), _ptr(r), _ptr(d),
+                                      _ptr(n), self._stream()), "oth_step_vs")
+        return (self.get_observation() if observe else None), r, d.bool(), n
+
     def legal_mask(self):
         """possible_moves of every board as (E, W) int64 bit masks (bit a = square a)."""
         out = torch.empty(self.num_envs, self.words, dtype=torch.int64, device=self.device)

@@ -96,6 +96,25 @@ int oth_step(oth_env *env, const int32_t *actions, int32_t *rewards, uint8_t *do
 int oth_step_policy(oth_env *env, int32_t policy, int32_t n_plies, int32_t *actions, int32_t *rewards,
                     uint8_t *dones, oth_stream_t stream);
 
+/* OthelloEnv (othello.py:96-214) for every env: the protagonist's colour per
+ * env (protagonist: device int8[E] of +1 white / -1 black, NULL = all white,
+ * the reference default) and an embedded opponent played on the device
+ * (OTH_POLICY_RANDOM / OTH_POLICY_GREEDY).
+ *   oth_reset_vs: OthelloEnv.reset (:151-174) -- reset, then the opponent
+ *     replies (with its policy) until the protagonist is to move.
+ *   oth_step_vs:  OthelloEnv.step (:176-200) -- the protagonist plays
+ *     actions[e] (a random move while random-opening plies remain), then the
+ *     opponent replies until the protagonist is to move again or the game
+ *     ends.  rewards[e] is the protagonist's step reward, negated when an
+ *     opponent ply ended the game (:200); plies[e] (may be NULL) counts the
+ *     plies applied.  With OTH_AUTO_RESET a finished env is reset_vs'd.
+ * Random draws: the j-th ply of call number c (the handle's ply counter,
+ * advanced by one per call) uses Philox block (c*256 + j) / 4, word (c*256 + j) % 4. */
+int oth_reset_vs(oth_env *env, int32_t opponent_policy, const int8_t *protagonist, const uint8_t *mask,
+                 oth_stream_t stream);
+int oth_step_vs(oth_env *env, int32_t opponent_policy, const int32_t *actions, const int8_t *protagonist,
+                int32_t *rewards, uint8_t *dones, int32_t *plies, oth_stream_t stream);
+
 /* possible_moves of every env as masks uint64[E][W] (othello.py:242, :270, :466). */
 int oth_legal(oth_env *env, uint64_t *out, oth_stream_t stream);
 

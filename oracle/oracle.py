@@ -44,6 +44,8 @@ def lib():
         L.oracle_greedy_batch.argtypes = [i32, i32, P, P, P, P]
         L.oracle_recompute_legal.argtypes = [i32, i32, P, P, P]
         L.oracle_observe.argtypes = [i32, i32, P, P, P, P, P, P]
+        L.oracle_reset_vs.argtypes = [i32, u32, i32, i32, u64, u32, u64, i32, P, P, P, P]
+        L.oracle_step_vs.argtypes = [i32, u32, i32, i32, u64, u32, u64, i32, P, P, P, P, P, P, P, P, P]
         _lib = L
     return _lib
 
@@ -151,3 +153,25 @@ def meta_from(turn, terminated=False, winner=0, rand_left=0):
     m |= (np.where(w == 1, 1, np.where(w == -1, 2, 0)).astype(np.uint16) << 2)
     m |= (np.asarray(rand_left).astype(np.uint16) << 8)
     return m.astype(np.uint16)
+
+
+def reset_vs(n, E, flags, policy, call, seed=0, id_base=0, initial_rand_steps=0, prot=None):
+    """OthelloEnv.reset for E boards (device semantics of oth_reset_vs)."""
+    s = State(n, E)
+    prot = None if prot is None else np.ascontiguousarray(prot, dtype=np.int8)
+    lib().oracle_reset_vs(n, flags, policy, initial_rand_steps, seed, id_base, call, E, _p(prot),
+                          _p(s.boards), _p(s.meta), _p(s.legal))
+    return s
+
+
+def step_vs(s, flags, policy, call, actions, seed=0, id_base=0, initial_rand_steps=0, prot=None, wdl=None):
+    """OthelloEnv.step for E boards in place; returns (rewards, dones, plies)."""
+    actions = np.ascontiguousarray(actions, dtype=np.int32)
+    prot = None if prot is None else np.ascontiguousarray(prot, dtype=np.int8)
+    rewards = np.zeros(s.E, dtype=np.int32)
+    dones = np.zeros(s.E, dtype=np.uint8)
+    plies = np.zeros(s.E, dtype=np.int32)
+    lib().oracle_step_vs(s.n, flags, policy, initial_rand_steps, seed, id_base, call, s.E, _p(prot),
+                         _p(actions), _p(s.boards), _p(s.meta), _p(s.legal), _p(rewards), _p(dones),
+                         _p(plies), _p(wdl))
+    return rewards, dones, plies

@@ -470,3 +470,93 @@ void oracle_observe(int n, int E, const uint64_t *boards, const uint16_t *meta, 
         }
     }
 }
+
+/* ---------------- OthelloEnv with an embedded opponent (othello.py:151-200) ---------------- */
+#define VS_PLIES_PER_CALL 256u
+
+/* while the game runs and it is not the protagonist's turn, the opponent moves
+ * (othello.py:190-199); `openings` applies the rand_step_cnt override (:191-194),
+ * which the opponent's reply inside reset() does not (:165-169). */
+static void opponent_reply(oenv *e, int prot, int openings, int policy, uint64_t seed, uint32_t id, uint64_t gbase,
+                           uint32_t *j, int *r, int *d) {
+    while (!e->terminated && e->turn != prot) {
+        uint64_t g = gbase + (*j)++; /* ply j of the call */
+        int a;
+        if (policy == 0 || (openings && e->rand_left > 0))
+            a = random_action(e, seed, id, g);
+        else
+            a = greedy_action(e);
+        if (openings && e->rand_left > 0) e->rand_left--;
+        env_step(e, a, r, d);
+    }
+}
+
+static void reset_vs(oenv *e, int prot, int policy, uint64_t seed, uint32_t id, uint64_t call, uint32_t purpose,
+                     int initial_rand_steps, uint32_t *j) {
+    int r, d;
+    env_reset(e);
+    e->rand_left = initial_rand_steps > 0 ? opening_plies(seed, id, call, purpose, initial_rand_steps) : 0;
+    opponent_reply(e, prot, 0, policy, seed, id, call * VS_PLIES_PER_CALL, j, &r, &d);
+}
+
+/* OthelloEnv.reset (othello.py:151-174) for E envs; prot int8[E] (+1/-1) or NULL = white. */
+void oracle_reset_vs(int n, uint32_t flags, int policy, int initial_rand_steps, uint64_t seed, uint32_t id_base,
+                     uint64_t call, int E, const int8_t *prot, uint64_t *boards, uint16_t *meta, uint64_t *legal) {
+    int W = nwords(n);
+    oenv e;
+    memset(&e, 0, sizeof(e));
+    e.n = n;
+    e.sudden_death = (flags & F_SUDDEN_DEATH) != 0;
+    e.disk_reward = (flags & F_DISK_REWARD) != 0;
+    for (int i = 0; i < E; i++) {
+        uint32_t j = 0;
+        reset_vs(&e, prot ? prot[i] : WHITE_DISK, policy, seed, id_base + (uint32_t)i, call, 2, initial_rand_steps, &j);
+        store(&e, boards + (size_t)i * 2 * W, meta + i, legal + (size_t)i * W);
+    }
+}
+
+/* OthelloEnv.step (othello.py:176-200) for E envs: rewards from the
+ * protagonist's view (negated after an opponent ply, :200). */
+void oracle_step_vs(int n, uint32_t flags, int policy, int initial_rand_steps, uint64_t seed, uint32_t id_base,
+                    uint64_t call, int E, const int8_t *prot, const int32_t *actions, uint64_t *boards,
+                    uint16_t *meta, uint64_t *legal, int32_t *rewards, uint8_t *dones, int32_t *plies,
+                    int64_t *wdl) {
+    int W = nwords(n);
+    oenv e;
+    for (int i = 0; i < E; i++) {
+        uint64_t *bd = boards + (size_t)i * 2 * W, *lg = legal + (size_t)i * W;
+        uint32_t id = id_base + (uint32_t)i, j = 0;
+        int p = prot ? prot[i] : WHITE_DISK;
+        uint64_t gbase = call * VS_PLIES_PER_CALL;
+        load(&e, n, flags, bd, meta[i], lg);
+        int r = 0, d = 1, np = 0;
+        if (!e.terminated) {
+            d = 0;
+            opponent_reply(&e, p, 1, policy, seed, id, gbase, &j, &r, &d);
+            if (!e.terminated) {
+                int a = actions[i];
+                uint64_t g = gbase + j++;
+                if (e.rand_left > 0) { /* :179-182 */
+                    a = random_action(&e, seed, id, g);
+                    e.rand_left--;
+                }
+                env_step(&e, a, &r, &d);
+                if (!d) {
+                    opponent_reply(&e, p, 1, policy, seed, id, gbase, &j, &r, &d);
+                    r = -r;
+                }
+            } else {
+                r = -r;
+            }
+            np = (int)j;
+            if (d) {
+                if (wdl) wdl[e.winner == BLACK_DISK ? 0 : (e.winner == NO_DISK ? 1 : 2)]++;
+                if (flags & F_AUTO_RESET) reset_vs(&e, p, policy, seed, id, call, 1, initial_rand_steps, &j);
+            }
+        }
+        store(&e, bd, meta + i, lg);
+        if (rewards) rewards[i] = r;
+        if (dones) dones[i] = (uint8_t)d;
+        if (plies) plies[i] = np;
+    }
+}

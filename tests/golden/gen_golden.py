@@ -297,6 +297,94 @@ def gen_wrappers(othello, simple_policies):
         json.dump(traces, f, separators=(",", ":"))
 
 
+class RawObsGreedy(object):
+    """simple_policies.GreedyPolicy's algorithm (simple_policies.py:69-92) with the
+    reference's own env machinery, fed the raw observation OthelloEnv passes
+    (GreedyPolicy itself expects make_state planes there and cannot run inside
+    OthelloEnv -- SURVEY.md §A.4)."""
+
+    def __init__(self, othello):
+        self.othello = othello
+        self.env = None
+
+    def reset(self, env):
+        self.env = env.env if hasattr(env, 'env') else env
+
+    def get_action(self, obs):
+        env = self.env
+        me = env.player_turn
+        sim = self.othello.OthelloBaseEnv(board_size=env.board_size,
+                                          sudden_death_on_invalid_move=env.sudden_death_on_invalid_move,
+                                          mute=True)
+        counts = []
+        for move in env.possible_moves:
+            sim.reset()
+            sim.set_board_state(env.board_state.copy(), perspective=1)
+            sim.set_player_turn(me)
+            sim.step(move)
+            w, b = sim.count_disks()
+            counts.append(w if me == 1 else b)
+        return env.possible_moves[int(np.argmax(counts))]
+
+
+def gen_vs(othello):
+    """OthelloEnv (othello.py:96-214) with a deterministic greedy opponent and
+    seeded protagonist actions (incl. invalid ones), initial_rand_steps = 0."""
+    out = {}
+    quiet = io.StringIO()
+    for n in (6, 8):
+        rec = {k: [] for k in ("combo", "game", "ply", "action", "reward", "done", "black", "white", "turn")}
+        starts = []
+        ci = 0
+        combos = []
+        for prot in (1, -1):
+            for sd in (True, False):
+                for dr in (False, True):
+                    combos.append((prot, sd, dr))
+                    opp = RawObsGreedy(othello)
+                    env = othello.OthelloEnv(white_policy=opp, black_policy=opp, protagonist=prot, board_size=n,
+                                             seed=0, initial_rand_steps=0, sudden_death_on_invalid_move=sd,
+                                             num_disk_as_reward=dr)
+                    rnd = np.random.RandomState(500 + 10 * n + ci)
+                    with contextlib.redirect_stdout(quiet):
+                        for g in range(8):
+                            env.reset()
+                            b, w, t, _ = snapshot(env.env, n)
+                            starts.append((ci, g, b, w, t))
+                            done, ply = False, 0
+                            while not done:
+                                pm = env.possible_moves
+                                if rnd.rand() < 0.03 or not pm:
+                                    a = int(rnd.randint(-1, n * n + 1))
+                                else:
+                                    a = int(pm[rnd.randint(0, len(pm))])
+                                _, r, done, _ = env.step(a)
+                                b, w, t, _ = snapshot(env.env, n)
+                                for k, v in (("combo", ci), ("game", g), ("ply", ply), ("action", a),
+                                             ("reward", int(r)), ("done", bool(done)), ("black", b),
+                                             ("white", w), ("turn", t)):
+                                    rec[k].append(v)
+                                ply += 1
+                    ci += 1
+        for k in ("black", "white"):
+            rec[k] = np.array(rec[k], dtype=np.uint64).reshape(-1, nwords(n))
+        out["N%d_combo" % n] = np.array(rec["combo"], dtype=np.int8)
+        out["N%d_game" % n] = np.array(rec["game"], dtype=np.int16)
+        out["N%d_ply" % n] = np.array(rec["ply"], dtype=np.int16)
+        out["N%d_action" % n] = np.array(rec["action"], dtype=np.int32)
+        out["N%d_reward" % n] = np.array(rec["reward"], dtype=np.int32)
+        out["N%d_done" % n] = np.array(rec["done"], dtype=bool)
+        out["N%d_black" % n] = rec["black"]
+        out["N%d_white" % n] = rec["white"]
+        out["N%d_turn" % n] = np.array(rec["turn"], dtype=np.int8)
+        out["N%d_combos" % n] = np.array(combos, dtype=np.int8)
+        out["N%d_start_black" % n] = np.array([s_[2] for s_ in starts], dtype=np.uint64)
+        out["N%d_start_white" % n] = np.array([s_[3] for s_ in starts], dtype=np.uint64)
+        out["N%d_start_turn" % n] = np.array([s_[4] for s_ in starts], dtype=np.int8)
+        print("vs N=%d: %d protagonist steps" % (n, len(rec["action"])))
+    np.savez_compressed(os.path.join(OUT, "vs_greedy.npz"), **out)
+
+
 def main():
     install_shims()
     import othello  # noqa: E402  (reference, read-only)
@@ -307,6 +395,7 @@ def main():
     gen_greedy(othello, simple_policies, util)
     gen_obs(othello, util)
     gen_wrappers(othello, simple_policies)
+    gen_vs(othello)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,74 @@
+// Host build of csrc/bitboard.hpp (the same templates the kernels use) for CPU
+// tests: legal_moves<N> / flips<N> / select_bit / philox4 exported with C linkage.
+// Built by tests/test_bitboard_host.py with g++; test infrastructure only.
+#include <stdint.h>
+#include <string.h>
+
+#include "../../gymothelloenv_amd/csrc/bitboard.hpp"
+
+using namespace oth;
+
+template <int N>
+static void legal_n(int E, const uint64_t* mover, const uint64_t* opp, uint64_t* out) {
+    constexpr int W = Geo<N>::W;
+    for (int e = 0; e < E; ++e) {
+        BB<W> P, O;
+        for (int i = 0; i < W; ++i) {
+            P.w[i] = mover[e * W + i];
+            O.w[i] = opp[e * W + i];
+        }
+        BB<W> L = legal_moves<N>(P, O);
+        memcpy(out + e * W, L.w, sizeof(L.w));
+    }
+}
+
+template <int N>
+static void flips_n(int E, const uint64_t* mover, const uint64_t* opp, const int32_t* sq, uint64_t* out) {
+    constexpr int W = Geo<N>::W;
+    for (int e = 0; e < E; ++e) {
+        BB<W> P, O;
+        for (int i = 0; i < W; ++i) {
+            P.w[i] = mover[e * W + i];
+            O.w[i] = opp[e * W + i];
+        }
+        BB<W> f = flips<N>(P, O, square<W>(sq[e]));
+        memcpy(out + e * W, f.w, sizeof(f.w));
+    }
+}
+
+#define DISPATCH(fn, ...)                \
+    switch (n) {                         \
+        case 4: fn<4>(__VA_ARGS__); break;   \
+        case 5: fn<5>(__VA_ARGS__); break;   \
+        case 6: fn<6>(__VA_ARGS__); break;   \
+        case 7: fn<7>(__VA_ARGS__); break;   \
+        case 8: fn<8>(__VA_ARGS__); break;   \
+        case 9: fn<9>(__VA_ARGS__); break;   \
+        case 10: fn<10>(__VA_ARGS__); break; \
+        case 11: fn<11>(__VA_ARGS__); break; \
+        case 12: fn<12>(__VA_ARGS__); break; \
+        case 13: fn<13>(__VA_ARGS__); break; \
+        case 14: fn<14>(__VA_ARGS__); break; \
+        case 15: fn<15>(__VA_ARGS__); break; \
+        case 16: fn<16>(__VA_ARGS__); break; \
+        default: return -1;              \
+    }
+
+extern "C" {
+int host_legal(int n, int E, const uint64_t* mover, const uint64_t* opp, uint64_t* out) {
+    DISPATCH(legal_n, E, mover, opp, out);
+    return 0;
+}
+int host_flips(int n, int E, const uint64_t* mover, const uint64_t* opp, const int32_t* sq, uint64_t* out) {
+    DISPATCH(flips_n, E, mover, opp, sq, out);
+    return 0;
+}
+int host_select(uint64_t x, int k) { return select64(x, k); }
+void host_philox4(uint64_t seed, uint32_t id, uint64_t ctr, uint32_t purpose, uint32_t* out) {
+    U4 u = philox4(seed, id, ctr, purpose);
+    out[0] = u.x;
+    out[1] = u.y;
+    out[2] = u.z;
+    out[3] = u.w;
+}
+}

@@ -1,0 +1,92 @@
+"""The kernels' bitboard algorithms (csrc/bitboard.hpp, compiled for the host
+with g++) against the oracle's cell-by-cell ray walk, on random boards of
+every size -- a CPU check of the exact code the GPU runs."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "host", "bitboard_host.cpp")
+LIB = os.path.join(HERE, "host", "libbitboard_host.so")
+HDR = os.path.join(os.path.dirname(HERE), "gymothelloenv_amd", "csrc", "bitboard.hpp")
+
+
+@pytest.fixture(scope="module")
+def hostlib():
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(SRC), os.path.getmtime(HDR)):
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", LIB, SRC])
+    L = ctypes.CDLL(LIB)
+    P = ctypes.c_void_p
+    L.host_legal.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P]
+    L.host_flips.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P]
+    L.host_select.argtypes = [ctypes.c_uint64, ctypes.c_int]
+    L.host_philox4.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32, P]
+    return L
+
+
+def ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def random_boards(n, E, rng, density):
+    W = oracle.nwords(n)
+    cells = rng.choice(3, size=(E, n * n), p=[1 - density, density / 2, density / 2])
+    mover = np.zeros((E, W), dtype=np.uint64)
+    opp = np.zeros((E, W), dtype=np.uint64)
+    for a in range(n * n):
+        mover[:, a // 64] |= (cells[:, a] == 1).astype(np.uint64) << np.uint64(a % 64)
+        opp[:, a // 64] |= (cells[:, a] == 2).astype(np.uint64) << np.uint64(a % 64)
+    return cells, mover, opp
+
+
+@pytest.mark.parametrize("n", list(range(4, 17)))
+def test_legal_moves_host_build(hostlib, n):
+    rng = np.random.RandomState(n)
+    for density in (0.3, 0.6, 0.9):
+        _, mover, opp = random_boards(n, 3000, rng, density)
+        out = np.zeros_like(mover)
+        assert hostlib.host_legal(n, len(mover), ptr(mover), ptr(opp), ptr(out)) == 0
+        np.testing.assert_array_equal(out, oracle.legal(n, mover, opp))
+
+
+@pytest.mark.parametrize("n", [4, 5, 6, 7, 8, 9, 10, 13, 16])
+def test_flips_host_build(hostlib, n):
+    """flips<N> from every legal square == the oracle's update_board diff."""
+    rng = np.random.RandomState(50 + n)
+    cells, mover, opp = random_boards(n, 1500, rng, 0.6)
+    legal = oracle.legal(n, mover, opp)
+    W = oracle.nwords(n)
+    sq = np.full(len(mover), -1, dtype=np.int32)
+    for e in range(len(mover)):
+        moves = [a for a in range(n * n) if (int(legal[e, a // 64]) >> (a % 64)) & 1]
+        if moves:
+            sq[e] = moves[rng.randint(len(moves))]
+    keep = sq >= 0
+    mover, opp, sq = mover[keep], opp[keep], sq[keep]
+    out = np.zeros_like(mover)
+    assert hostlib.host_flips(n, len(mover), ptr(mover), ptr(opp), ptr(sq), ptr(out)) == 0
+    # oracle: step the move as white (= mover) and diff the opponent's discs
+    s = oracle.State(n, len(mover))
+    s.boards[:] = np.concatenate([opp, mover], axis=1)   # black = opp, white = mover
+    s.meta[:] = oracle.meta_from(np.ones(len(mover)))
+    s.legal[:] = oracle.recompute_legal(s)
+    oracle.step(s, 0, sq)
+    np.testing.assert_array_equal(out, opp & ~s.boards[:, :W])
+
+
+def test_select_and_philox(hostlib):
+    rng = np.random.RandomState(0)
+    for _ in range(2000):
+        x = int(rng.randint(1, 2 ** 62, dtype=np.int64)) | (int(rng.randint(0, 2)) << 63)
+        bits = [i for i in range(64) if (x >> i) & 1]
+        k = int(rng.randint(len(bits)))
+        assert hostlib.host_select(x, k) == bits[k]
+    # Philox4x32-10 known-answer vector (Random123 kat_vectors: ctr 0, key 0)
+    out = np.zeros(4, dtype=np.uint32)
+    hostlib.host_philox4(0, 0, 0, 0, ptr(out))
+    assert [hex(v) for v in out] == ["0x6627e8d5", "0xe169c58d", "0xbc57ac4c", "0x9b00dbd8"]

@@ -294,3 +294,70 @@ def test_state_dict_roundtrip(torch_cuda):
     x, _, _ = a.step_policy("random", n_plies=50)
     y, _, _ = b.step_policy("random", n_plies=50)
     assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("n", [6, 8])
+def test_vs_greedy_matches_reference(torch_cuda, golden_dir, n):
+    """Device OthelloEnv (oth_reset_vs / oth_step_vs, greedy opponent) replays the
+    reference's OthelloEnv games in lockstep (finished games are no-ops)."""
+    torch = torch_cuda
+    v = np.load(os.path.join(golden_dir, "vs_greedy.npz"))
+    W = oracle.nwords(n)
+    for ci, (prot, sd, dr) in enumerate(v["N%d_combos" % n]):
+        sel = v["N%d_combo" % n] == ci
+        games = np.unique(v["N%d_game" % n][sel])
+        idx = [np.flatnonzero(sel & (v["N%d_game" % n] == g)) for g in games]
+        env = make_env(torch, len(games), n, sd=bool(sd), dr=bool(dr))
+        env.reset_vs("greedy", protagonist=int(prot))
+        b, _, _ = get_state_np(env)
+        n_games = len(games)
+        np.testing.assert_array_equal(b[:, :W], v["N%d_start_black" % n][ci * n_games:(ci + 1) * n_games])
+        np.testing.assert_array_equal(b[:, W:], v["N%d_start_white" % n][ci * n_games:(ci + 1) * n_games])
+        for p in range(max(len(i) for i in idx)):
+            acts = np.array([v["N%d_action" % n][i[p]] if p < len(i) else 0 for i in idx], dtype=np.int32)
+            _, rew, dn, plies = env.step_vs(torch.from_numpy(acts).cuda(), "greedy", observe=False)
+            b, m, _ = get_state_np(env)
+            rew, dn = rew.cpu().numpy(), dn.cpu().numpy()
+            for gi, i in enumerate(idx):
+                if p < len(i):
+                    k = i[p]
+                    assert rew[gi] == v["N%d_reward" % n][k] and bool(dn[gi]) == bool(v["N%d_done" % n][k])
+                    assert list(b[gi, :W]) == list(v["N%d_black" % n][k])
+                    assert list(b[gi, W:]) == list(v["N%d_white" % n][k])
+                    assert (1 if m[gi] & 1 else -1) == v["N%d_turn" % n][k]
+                else:
+                    assert dn[gi] and rew[gi] == 0
+
+
+@pytest.mark.parametrize("n,opp,init_rand", [(8, "random", 0), (8, "random", 10), (8, "greedy", 6), (6, "greedy", 0),
+                                              (10, "random", 4)])
+def test_vs_rollout_replays_on_oracle(torch_cuda, n, opp, init_rand):
+    """Mixed protagonist colours, random openings and auto-reset: every call's
+    rewards / dones / plies, the final state and the W/D/L tally equal the oracle."""
+    torch = torch_cuda
+    E, calls = 4096, 80
+    pol = 0 if opp == "random" else 1
+    prot = np.where(np.arange(E) % 3 == 0, -1, 1).astype(np.int8)
+    env = make_env(torch, E, n, auto=True, seed=13, init_rand=init_rand)
+    env.reset_vs(opp, protagonist=torch.from_numpy(prot))
+    flags = flags_of(True, False, True)
+    s = oracle.reset_vs(n, E, flags, pol, 0, seed=13, initial_rand_steps=init_rand, prot=prot)
+    b, m, lg = get_state_np(env)
+    np.testing.assert_array_equal(b, s.boards)
+    np.testing.assert_array_equal(m, s.meta)
+    rng = np.random.RandomState(n)
+    wdl = np.zeros(3, dtype=np.int64)
+    for c in range(1, calls + 1):
+        lb = legal_bool(s.legal, n)
+        pick = np.argmax(rng.rand(E, n * n) * lb, axis=1).astype(np.int32)
+        acts = np.where((rng.rand(E) < 0.02) | ~lb.any(axis=1), rng.randint(-1, n * n, size=E), pick).astype(np.int32)
+        orw, od, opl = oracle.step_vs(s, flags, pol, c, acts, seed=13, initial_rand_steps=init_rand, prot=prot, wdl=wdl)
+        _, rew, dn, plies = env.step_vs(torch.from_numpy(acts).cuda(), opp, observe=False)
+        np.testing.assert_array_equal(rew.cpu().numpy(), orw)
+        np.testing.assert_array_equal(dn.cpu().numpy(), od.astype(bool))
+        np.testing.assert_array_equal(plies.cpu().numpy(), opl)
+    b, m, lg = get_state_np(env)
+    np.testing.assert_array_equal(b, s.boards)
+    np.testing.assert_array_equal(m, s.meta)
+    np.testing.assert_array_equal(lg, s.legal)
+    np.testing.assert_array_equal(env.counts().cpu().numpy(), wdl)

@@ -148,3 +148,31 @@ def test_random_policy_distribution():
     assert wdl.sum() == 2000  # every 8x8 random game ends within 60 + passes <= 64 plies
     frac = wdl / wdl.sum()
     assert 0.40 < frac[0] < 0.52 and 0.02 < frac[1] < 0.08 and 0.43 < frac[2] < 0.56
+
+
+def vs_flags(sd, dr):
+    return (oracle.F_SUDDEN_DEATH if sd else 0) | (oracle.F_DISK_REWARD if dr else 0)
+
+
+@pytest.mark.parametrize("n", [6, 8])
+def test_vs_greedy_matches_reference(golden_dir, n):
+    """OthelloEnv semantics (othello.py:151-200) with a greedy opponent: the
+    oracle's reset_vs/step_vs replay the reference's recorded games."""
+    v = np.load(os.path.join(golden_dir, "vs_greedy.npz"))
+    combos = v["N%d_combos" % n]
+    W = oracle.nwords(n)
+    starts = 0
+    for ci, (prot, sd, dr) in enumerate(combos):
+        sel = v["N%d_combo" % n] == ci
+        for g in np.unique(v["N%d_game" % n][sel]):
+            idx = np.flatnonzero(sel & (v["N%d_game" % n] == g))
+            s = oracle.reset_vs(n, 1, vs_flags(sd, dr), 1, 0, prot=[prot])
+            assert list(s.boards[0, :W]) == list(v["N%d_start_black" % n][starts])
+            assert list(s.boards[0, W:]) == list(v["N%d_start_white" % n][starts])
+            starts += 1
+            for k, i in enumerate(idx):
+                r, d, plies = oracle.step_vs(s, vs_flags(sd, dr), 1, k + 1, [v["N%d_action" % n][i]], prot=[prot])
+                assert r[0] == v["N%d_reward" % n][i] and bool(d[0]) == bool(v["N%d_done" % n][i])
+                assert list(s.boards[0]) == list(v["N%d_black" % n][i]) + list(v["N%d_white" % n][i])
+                assert (1 if s.meta[0] & 1 else -1) == v["N%d_turn" % n][i]
+                assert plies[0] >= 1

@@ -31,7 +31,7 @@ def build(specs):
         subprocess.check_call(cmd)
 
 
-def run(names, E, n, plies, launches, rounds, policy):
+def run(names, E, n, plies, launches, rounds, policy, check=True):
     import torch
 
     from gymothelloenv_amd import _lib as L
@@ -42,6 +42,8 @@ def run(names, E, n, plies, launches, rounds, policy):
     # correctness: identical trajectories
     ref = None
     for nm, env in envs.items():
+        if not check:
+            break
         a, _, _ = env.step_policy(policy, n_plies=plies)
         st = [t.clone() for t in env.get_state()]
         if ref is None:
@@ -84,11 +86,12 @@ def main():
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--policy", default="random")
+    ap.add_argument("--no-check", action="store_true", help="timing ablations: outputs differ by design")
     a = ap.parse_args()
     if a.build:
         build(a.build)
     if a.run:
-        run(a.run, a.envs, a.board_size, a.plies, a.launches, a.rounds, a.policy)
+        run(a.run, a.envs, a.board_size, a.plies, a.launches, a.rounds, a.policy, check=not a.no_check)
 
 
 if __name__ == "__main__":
