@@ -8,7 +8,7 @@ terminal/score) as HIP kernels for gfx950 behind a C ABI
     OthelloBaseEnv,          drop-in single-board classes with the
     SimpleOthelloEnv,        reference's constructor / attributes / 4-tuple step
     OthelloEnv
-    RandomPolicy, GreedyPolicy, make_state, undo_state
+    RandomPolicy, GreedyPolicy, MaxiMinPolicy, make_state, undo_state
 """
 from ._lib import LIB_PATH, OthelloLibError, load  # noqa: F401
 
@@ -23,7 +23,7 @@ def __getattr__(name):
     if name in ("OthelloBaseEnv", "SimpleOthelloEnv", "OthelloEnv"):
         from . import othello
         return getattr(othello, name)
-    if name in ("RandomPolicy", "GreedyPolicy"):
+    if name in ("RandomPolicy", "GreedyPolicy", "MaxiMinPolicy"):
         from . import policies
         return getattr(policies, name)
     if name in ("make_state", "undo_state"):

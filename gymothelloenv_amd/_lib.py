@@ -19,6 +19,9 @@ OTH_DISK_REWARD = 2
 OTH_AUTO_RESET = 4
 OTH_POLICY_RANDOM = 0
 OTH_POLICY_GREEDY = 1
+OTH_POLICY_MAXIMIN1 = 2
+OTH_POLICY_MAXIMIN2 = 3
+OTH_POLICY_MAXIMIN3 = 4
 OTH_OBS_BOARD = 0
 OTH_OBS_BOARD_LEGAL = 1
 OTH_OBS_MAKE_STATE = 2
@@ -39,6 +42,7 @@ SIGNATURES = {
     "oth_legal": (_I32, [_P, _P, _P]),
     "oth_legal_moves": (_I32, [_I32, _I32, _P, _P, _P, _P]),
     "oth_greedy_actions": (_I32, [_P, _P, _P]),
+    "oth_policy_actions": (_I32, [_P, _I32, _P, _P]),
     "oth_observe": (_I32, [_P, _I32, _I32, _P, _P]),
     "oth_get_state": (_I32, [_P, _P, _P, _P, _P]),
     "oth_set_state": (_I32, [_P, _P, _P, _P, _P]),

@@ -1,0 +1,343 @@
+// capi.hip -- the C ABI declared in include/othello_mi355x.h: argument checks,
+// handle lifetime, error reporting and dispatch on the board size to the
+// per-N launchers (kernels_n.hip).
+#include <hip/hip_runtime.h>
+
+#include <stdio.h>
+#include <string.h>
+
+#include <new>
+#include <string>
+#include <type_traits>
+
+#include "device.hpp"
+#include "launch.hpp"
+
+using namespace oth;
+using namespace oth_dev;
+using namespace oth_host;
+
+namespace oth_host {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* msg) {
+    g_last_error = msg;
+    return code;
+}
+
+int hip_fail(hipError_t err, const char* where) {
+    char buf[256];
+    snprintf(buf, sizeof(buf), "%s: %s", where, hipGetErrorString(err));
+    g_last_error = buf;
+    return OTH_EHIP;
+}
+
+int after_launch(const char* what) {
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return hip_fail(err, what);
+    return OTH_OK;
+}
+
+}  // namespace oth_host
+
+namespace {
+
+#define OTH_HIP(call)                                         \
+    do {                                                      \
+        hipError_t err_ = (call);                             \
+        if (err_ != hipSuccess) return hip_fail(err_, #call); \
+    } while (0)
+
+template <typename Fn>
+int with_n(int n, Fn&& fn) {
+    switch (n) {
+        case 4: return fn(std::integral_constant<int, 4>{});
+        case 5: return fn(std::integral_constant<int, 5>{});
+        case 6: return fn(std::integral_constant<int, 6>{});
+        case 7: return fn(std::integral_constant<int, 7>{});
+        case 8: return fn(std::integral_constant<int, 8>{});
+        case 9: return fn(std::integral_constant<int, 9>{});
+        case 10: return fn(std::integral_constant<int, 10>{});
+        case 11: return fn(std::integral_constant<int, 11>{});
+        case 12: return fn(std::integral_constant<int, 12>{});
+        case 13: return fn(std::integral_constant<int, 13>{});
+        case 14: return fn(std::integral_constant<int, 14>{});
+        case 15: return fn(std::integral_constant<int, 15>{});
+        case 16: return fn(std::integral_constant<int, 16>{});
+        default: return fail(OTH_EINVAL, "board_size must be in [4, 16]");
+    }
+}
+
+int use_device(const oth_env* env) {
+    int cur = -1;
+    OTH_HIP(hipGetDevice(&cur));
+    if (cur != env->device) OTH_HIP(hipSetDevice(env->device));
+    return OTH_OK;
+}
+
+#define OTH_CHECK_ENV(env)                                    \
+    do {                                                      \
+        if (!(env)) return fail(OTH_EINVAL, "NULL oth_env");  \
+        int rc_ = use_device(env);                            \
+        if (rc_) return rc_;                                  \
+    } while (0)
+
+// oth_counts: sum the per-block slots into out[3] (int64); optionally zero them.
+__global__ __launch_bounds__(256) void k_reduce_wdl(unsigned long long* __restrict__ wdl, int nslots,
+                                                   int64_t* __restrict__ out, int reset) {
+    __shared__ unsigned long long acc[256][3];
+    unsigned long long b = 0, d = 0, w = 0;
+    for (int i = threadIdx.x; i < nslots; i += 256) {
+        b += wdl[4 * (size_t)i];
+        d += wdl[4 * (size_t)i + 1];
+        w += wdl[4 * (size_t)i + 2];
+        if (reset) {
+            wdl[4 * (size_t)i] = 0;
+            wdl[4 * (size_t)i + 1] = 0;
+            wdl[4 * (size_t)i + 2] = 0;
+        }
+    }
+    acc[threadIdx.x][0] = b;
+    acc[threadIdx.x][1] = d;
+    acc[threadIdx.x][2] = w;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) {
+            acc[threadIdx.x][0] += acc[threadIdx.x + s][0];
+            acc[threadIdx.x][1] += acc[threadIdx.x + s][1];
+            acc[threadIdx.x][2] += acc[threadIdx.x + s][2];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < 3) out[threadIdx.x] = (int64_t)acc[0][threadIdx.x];
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* oth_last_error(void) { return g_last_error.c_str(); }
+
+const char* oth_version(void) { return "othello_mi355x 0.1 (gfx950)"; }
+
+int oth_create(int32_t n_envs, int32_t board_size, uint32_t flags, uint64_t seed, uint32_t env_id_base,
+               int32_t initial_rand_steps, int32_t device, oth_env** out) {
+    if (!out) return fail(OTH_EINVAL, "out is NULL");
+    *out = nullptr;
+    if (n_envs <= 0) return fail(OTH_EINVAL, "n_envs must be > 0");
+    const int n = board_size < 4 ? 4 : board_size;  // othello.py:230
+    if (n > 16) return fail(OTH_EINVAL, "board_size must be <= 16");
+    if (initial_rand_steps < 0 || initial_rand_steps > 255)
+        return fail(OTH_EINVAL, "initial_rand_steps must be in [0, 255]");
+    if (flags & ~7u) return fail(OTH_EINVAL, "unknown flag bits");
+    OTH_HIP(hipSetDevice(device));
+    oth_env* env = new (std::nothrow) oth_env();
+    if (!env) return fail(OTH_ENOMEM, "host allocation failed");
+    env->E = n_envs;
+    env->n = n;
+    env->W = (n * n + 63) / 64;
+    env->flags = flags;
+    env->seed = seed;
+    env->id_base = env_id_base;
+    env->init_rand = initial_rand_steps;
+    env->device = device;
+    env->ply = 0;
+    const size_t E = (size_t)n_envs, W = (size_t)env->W;
+    hipError_t err = hipMalloc((void**)&env->boards, E * 2 * W * sizeof(uint64_t));
+    if (err == hipSuccess) err = hipMalloc((void**)&env->meta, ((E * sizeof(uint16_t) + 15) / 16) * 16);
+    if (err == hipSuccess) err = hipMalloc((void**)&env->legal, E * W * sizeof(uint64_t));
+    env->nslots = (int32_t)((2 * E + BLOCK - 1) / BLOCK);  // the widest grid (Pair: 2 lanes per board)
+    const size_t slot_bytes = (size_t)env->nslots * 4 * sizeof(unsigned long long);
+    if (err == hipSuccess) err = hipMalloc((void**)&env->wdl, slot_bytes);
+    if (err == hipSuccess) err = hipMemset(env->wdl, 0, slot_bytes);
+    if (err != hipSuccess) {
+        oth_destroy(env);
+        return hip_fail(err, "oth_create: allocation");
+    }
+    int rc = oth_reset(env, nullptr, nullptr);
+    if (rc == OTH_OK) {
+        err = hipStreamSynchronize(nullptr);
+        if (err != hipSuccess) rc = hip_fail(err, "oth_create: reset");
+    }
+    if (rc != OTH_OK) {
+        oth_destroy(env);
+        return rc;
+    }
+    *out = env;
+    return OTH_OK;
+}
+
+int oth_destroy(oth_env* env) {
+    if (!env) return OTH_OK;
+    (void)hipSetDevice(env->device);
+    if (env->boards) (void)hipFree(env->boards);
+    if (env->meta) (void)hipFree(env->meta);
+    if (env->legal) (void)hipFree(env->legal);
+    if (env->wdl) (void)hipFree(env->wdl);
+    delete env;
+    return OTH_OK;
+}
+
+int oth_reset(oth_env* env, const uint8_t* mask, oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    return with_n(env->n, [&](auto NC) { return launch_reset<decltype(NC)::value>(env, mask, (hipStream_t)stream); });
+}
+
+int oth_step(oth_env* env, const int32_t* actions, int32_t* rewards, uint8_t* dones, oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    if (!actions) return fail(OTH_EINVAL, "actions is NULL");
+    const uint64_t ply = env->ply++;
+    return with_n(env->n, [&](auto NC) {
+        return launch_step<decltype(NC)::value>(env, actions, rewards, dones, ply, (hipStream_t)stream);
+    });
+}
+
+int oth_step_policy(oth_env* env, int32_t policy, int32_t n_plies, int32_t* actions, int32_t* rewards,
+                    uint8_t* dones, oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    if (n_plies < 0) return fail(OTH_EINVAL, "n_plies must be >= 0");
+    if (policy < OTH_POLICY_RANDOM || policy > OTH_POLICY_MAXIMIN3) return fail(OTH_EINVAL, "unknown policy");
+    if (n_plies == 0) return OTH_OK;
+    const uint64_t ply0 = env->ply;
+    env->ply += (uint64_t)n_plies;
+    return with_n(env->n, [&](auto NC) {
+        return launch_play<decltype(NC)::value>(env, policy, n_plies, actions, rewards, dones, ply0,
+                                                (hipStream_t)stream);
+    });
+}
+
+int oth_reset_vs(oth_env* env, int32_t opponent_policy, const int8_t* protagonist, const uint8_t* mask,
+                 oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    if (opponent_policy < OTH_POLICY_RANDOM || opponent_policy > OTH_POLICY_MAXIMIN3)
+        return fail(OTH_EINVAL, "unknown opponent policy");
+    const uint64_t call = env->ply++;
+    return with_n(env->n, [&](auto NC) {
+        return launch_reset_vs<decltype(NC)::value>(env, opponent_policy, protagonist, mask, call,
+                                                    (hipStream_t)stream);
+    });
+}
+
+int oth_step_vs(oth_env* env, int32_t opponent_policy, const int32_t* actions, const int8_t* protagonist,
+                int32_t* rewards, uint8_t* dones, int32_t* plies, oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    if (!actions) return fail(OTH_EINVAL, "actions is NULL");
+    if (opponent_policy < OTH_POLICY_RANDOM || opponent_policy > OTH_POLICY_MAXIMIN3)
+        return fail(OTH_EINVAL, "unknown opponent policy");
+    const uint64_t call = env->ply++;
+    return with_n(env->n, [&](auto NC) {
+        return launch_step_vs<decltype(NC)::value>(env, opponent_policy, actions, protagonist, rewards, dones,
+                                                   plies, call, (hipStream_t)stream);
+    });
+}
+
+int oth_policy_actions(oth_env* env, int32_t policy, int32_t* out, oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    if (!out) return fail(OTH_EINVAL, "out is NULL");
+    if (policy < OTH_POLICY_GREEDY || policy > OTH_POLICY_MAXIMIN3)
+        return fail(OTH_EINVAL, "policy must be greedy or maximin");
+    return with_n(env->n, [&](auto NC) {
+        return launch_policy_actions<decltype(NC)::value>(env, policy, out, (hipStream_t)stream);
+    });
+}
+
+int oth_greedy_actions(oth_env* env, int32_t* out, oth_stream_t stream) {
+    return oth_policy_actions(env, OTH_POLICY_GREEDY, out, stream);
+}
+
+int oth_legal(oth_env* env, uint64_t* out, oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    if (!out) return fail(OTH_EINVAL, "out is NULL");
+    OTH_HIP(hipMemcpyAsync(out, env->legal, (size_t)env->E * env->W * sizeof(uint64_t), hipMemcpyDeviceToDevice,
+                           (hipStream_t)stream));
+    return OTH_OK;
+}
+
+int oth_legal_moves(int32_t board_size, int32_t n, const uint64_t* mover, const uint64_t* opp, uint64_t* out,
+                    oth_stream_t stream) {
+    if (n < 0 || (n > 0 && (!mover || !opp || !out))) return fail(OTH_EINVAL, "bad arguments");
+    if (n == 0) return OTH_OK;
+    const int bs = board_size < 4 ? 4 : board_size;
+    return with_n(bs, [&](auto NC) {
+        return launch_legal_moves<decltype(NC)::value>(n, mover, opp, out, (hipStream_t)stream);
+    });
+}
+
+
+int oth_observe(oth_env* env, int32_t layout, int32_t dtype, void* out, oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    if (!out) return fail(OTH_EINVAL, "out is NULL");
+    if (layout < OTH_OBS_BOARD || layout > OTH_OBS_ABSOLUTE) return fail(OTH_EINVAL, "unknown layout");
+    if (dtype < OTH_I8 || dtype > OTH_F64) return fail(OTH_EINVAL, "unknown dtype");
+    return with_n(env->n, [&](auto NC) {
+        return launch_observe<decltype(NC)::value>(env, layout, dtype, out, (hipStream_t)stream);
+    });
+}
+
+int oth_get_state(oth_env* env, uint64_t* boards, uint16_t* meta, uint64_t* legal, oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    const size_t E = (size_t)env->E, W = (size_t)env->W;
+    hipStream_t s = (hipStream_t)stream;
+    if (boards) OTH_HIP(hipMemcpyAsync(boards, env->boards, E * 2 * W * 8, hipMemcpyDefault, s));
+    if (meta) OTH_HIP(hipMemcpyAsync(meta, env->meta, E * 2, hipMemcpyDefault, s));
+    if (legal) OTH_HIP(hipMemcpyAsync(legal, env->legal, E * W * 8, hipMemcpyDefault, s));
+    return OTH_OK;
+}
+
+int oth_set_state(oth_env* env, const uint64_t* boards, const uint16_t* meta, const uint64_t* legal,
+                  oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    const size_t E = (size_t)env->E, W = (size_t)env->W;
+    hipStream_t s = (hipStream_t)stream;
+    if (boards) OTH_HIP(hipMemcpyAsync(env->boards, boards, E * 2 * W * 8, hipMemcpyDefault, s));
+    if (meta) OTH_HIP(hipMemcpyAsync(env->meta, meta, E * 2, hipMemcpyDefault, s));
+    if (legal) OTH_HIP(hipMemcpyAsync(env->legal, legal, E * W * 8, hipMemcpyDefault, s));
+    return OTH_OK;
+}
+
+int oth_set_player_turn(oth_env* env, int32_t turn, const uint8_t* mask, oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    if (turn != WHITE_DISK && turn != BLACK_DISK) return fail(OTH_EINVAL, "turn must be +1 or -1");
+    return with_n(env->n, [&](auto NC) {
+        return launch_set_turn<decltype(NC)::value>(env, turn, mask, (hipStream_t)stream);
+    });
+}
+
+int oth_count_disks(oth_env* env, int32_t* out, oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    if (!out) return fail(OTH_EINVAL, "out is NULL");
+    return with_n(env->n, [&](auto NC) { return launch_count<decltype(NC)::value>(env, out, (hipStream_t)stream); });
+}
+
+int oth_counts(oth_env* env, int64_t* out, int32_t reset, oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    if (!out) return fail(OTH_EINVAL, "out is NULL");
+    hipStream_t s = (hipStream_t)stream;
+#if OTH_TALLY_SLOTS
+    hipLaunchKernelGGL(k_reduce_wdl, dim3(1), dim3(256), 0, s, env->wdl, env->nslots, out, reset ? 1 : 0);
+    return after_launch("oth_counts");
+#else
+    OTH_HIP(hipMemcpyAsync(out, env->wdl, 3 * sizeof(int64_t), hipMemcpyDefault, s));
+    if (reset) OTH_HIP(hipMemsetAsync(env->wdl, 0, 4 * sizeof(unsigned long long), s));
+    return OTH_OK;
+#endif
+}
+
+uint64_t oth_ply_counter(const oth_env* env) { return env ? env->ply : 0; }
+
+int oth_set_ply_counter(oth_env* env, uint64_t ply) {
+    if (!env) return fail(OTH_EINVAL, "NULL oth_env");
+    env->ply = ply;
+    return OTH_OK;
+}
+
+int oth_shape(const oth_env* env, int32_t* n_envs, int32_t* board_size, int32_t* words) {
+    if (!env) return fail(OTH_EINVAL, "NULL oth_env");
+    if (n_envs) *n_envs = env->E;
+    if (board_size) *board_size = env->n;
+    if (words) *words = env->W;
+    return OTH_OK;
+}
+
+}  // extern "C"

@@ -1,6 +1,9 @@
-// othello_kernels.hip -- HIP/CDNA4 kernels of the vectorised Othello rules
-// engine and the C ABI declared in include/othello_mi355x.h.
+// device.hpp -- HIP/CDNA4 device code of the vectorised Othello rules engine:
+// per-lane board state, the rule engines (Solo / Rays / Pair), policies and
+// every __global__ kernel template.  Included by kernels_n.hip (compiled once
+// per board size N, so the templates build in parallel) and by capi.hip.
 //
+
 // One board per lane.  A board is two W-word bitboards (black, white) held in
 // VGPRs; legal moves and flips are Kogge-Stone occluded fills (bitboard.hpp).
 // The reference's per-step Python work -- get_possible_actions'
@@ -11,6 +14,7 @@
 // HBM layout (exchange format, see the header): boards [E][2W] u64 (a lane
 // reads 16W contiguous bytes: dwordx4 loads), meta [E] u16, legal [E][W] u64;
 // per-ply outputs are [ply][E] so every store instruction is coalesced.
+#pragma once
 #include <hip/hip_runtime.h>
 
 #include <stdio.h>
@@ -35,7 +39,7 @@ using namespace oth;
 #define OTH_BLOCK 256
 #endif
 
-namespace {
+namespace oth_dev {
 
 constexpr int BLOCK = OTH_BLOCK;
 constexpr uint32_t M_TURN_WHITE = 1u;
@@ -138,8 +142,8 @@ struct Solo {
 // Ray tables for one-word boards: rays[d*64 + sq] = the squares strictly beyond
 // sq in direction d, up to the edge.  d 0..3 point to higher squares (E, S, SE,
 // SW), d 4..7 to lower ones (W, N, NW, NE).  Built in LDS once per launch.
-__device__ __constant__ const int RAY_DR[8] = {0, 1, 1, 1, 0, -1, -1, -1};
-__device__ __constant__ const int RAY_DC[8] = {1, 0, 1, -1, -1, 0, -1, 1};
+static __device__ __constant__ const int RAY_DR[8] = {0, 1, 1, 1, 0, -1, -1, -1};
+static __device__ __constant__ const int RAY_DC[8] = {1, 0, 1, -1, -1, 0, -1, 1};
 
 template <int N>
 __device__ __forceinline__ void fill_rays(uint64_t* rays) {
@@ -423,6 +427,73 @@ __device__ __forceinline__ int greedy_action(const Lane<N>& s, const Eng& eng) {
     return best;
 }
 
+// MaxiMinPolicy(depth).get_action (simple_policies.py:98-163).  P is the side to
+// move at this node, O the other side; the root mover's ("my") discs are P at
+// even levels and O at odd ones.  A child is a leaf when the search depth is
+// reached, the board is full, or the side to reply has no move: the
+// reference then either ends the game (double pass) or forces the turn to
+// that side anyway (:139-144), whose empty move list ends the branch
+// (:117-126) -- either way the leaf value is my disc count.  Ties keep the
+// first (lowest) square: np.argmax / np.argmin (:152-154).  The depth is a
+// template parameter, so the recursion unrolls into straight-line levels.
+template <int N, int D, int LVL>
+__device__ int maximin_node(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O, const BB<Geo<N>::W>& L, int& move) {
+    constexpr int W = Geo<N>::W;
+    constexpr bool MINE = (LVL % 2) == 0;
+    int best = MINE ? -1 : 0x7fffffff;
+    move = -1;
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+        uint64_t x = L.w[i];
+        while (x) {
+            const int b = __builtin_ctzll(x);
+            x &= x - 1;
+            BB<W> m = zero<W>();
+            m.w[i] = 1ull << b;
+            const BB<W> f = flips<N>(P, O, m);
+            const BB<W> P2 = P | f | m;
+            const BB<W> O2 = O & ~(f | m);
+            int v = popcount(MINE ? P2 : O2);
+            if constexpr (LVL + 1 < D) {
+                if (any(~(P2 | O2) & Geo<N>::BOARD)) {
+                    const BB<W> L2 = legal_moves<N>(O2, P2);
+                    if (any(L2)) {
+                        int unused;
+                        v = maximin_node<N, D, LVL + 1>(O2, P2, L2, unused);
+                    }
+                }
+            }
+            if (MINE ? v > best : v < best) {
+                best = v;
+                move = 64 * i + b;
+            }
+        }
+    }
+    return best;
+}
+
+template <int N, int D>
+__device__ __forceinline__ int maximin_action(const Lane<N>& s) {
+    const bool tw = (s.meta & M_TURN_WHITE) != 0;
+    int move;
+    maximin_node<N, D, 0>(tw ? s.white : s.black, tw ? s.black : s.white, s.legal, move);
+    return move;
+}
+
+// The move of a deterministic scripted policy (everything but RANDOM).
+template <int N, int POLICY, typename Eng>
+__device__ __forceinline__ int policy_action(const Lane<N>& s, const Eng& eng) {
+    if constexpr (POLICY == OTH_POLICY_GREEDY) {
+        return greedy_action<N>(s, eng);
+    } else if constexpr (POLICY == OTH_POLICY_MAXIMIN2) {
+        return maximin_action<N, 2>(s);
+    } else if constexpr (POLICY == OTH_POLICY_MAXIMIN3) {
+        return maximin_action<N, 3>(s);
+    } else {
+        return -1;
+    }
+}
+
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -472,36 +543,6 @@ __device__ __forceinline__ void tally(unsigned long long* wdl, uint32_t b, uint3
         if (w) atomicAdd(wdl + 2, (unsigned long long)w);
     }
 #endif
-}
-
-// oth_counts: sum the per-block slots into out[3] (int64); optionally zero them.
-__global__ __launch_bounds__(256) void k_reduce_wdl(unsigned long long* __restrict__ wdl, int nslots,
-                                                   int64_t* __restrict__ out, int reset) {
-    __shared__ unsigned long long acc[256][3];
-    unsigned long long b = 0, d = 0, w = 0;
-    for (int i = threadIdx.x; i < nslots; i += 256) {
-        b += wdl[4 * (size_t)i];
-        d += wdl[4 * (size_t)i + 1];
-        w += wdl[4 * (size_t)i + 2];
-        if (reset) {
-            wdl[4 * (size_t)i] = 0;
-            wdl[4 * (size_t)i + 1] = 0;
-            wdl[4 * (size_t)i + 2] = 0;
-        }
-    }
-    acc[threadIdx.x][0] = b;
-    acc[threadIdx.x][1] = d;
-    acc[threadIdx.x][2] = w;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) {
-            acc[threadIdx.x][0] += acc[threadIdx.x + s][0];
-            acc[threadIdx.x][1] += acc[threadIdx.x + s][1];
-            acc[threadIdx.x][2] += acc[threadIdx.x + s][2];
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x < 3) out[threadIdx.x] = (int64_t)acc[0][threadIdx.x];
 }
 
 struct Rng {
@@ -597,7 +638,7 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
 #endif
                     if (rl > 0) s.meta -= 1u << M_RAND_SHIFT;
                 } else {
-                    a = greedy_action<N>(s, eng);
+                    a = policy_action<N, POLICY>(s, eng);
                 }
                 step_lane<N>(s, a, flags, r, d, win, eng);
                 if (d) {
@@ -647,7 +688,7 @@ __device__ __forceinline__ void opponent_reply(Lane<N>& s, bool prot_white, bool
         if (POLICY == OTH_POLICY_RANDOM || (openings && rl > 0)) {
             a = random_action<N>(s, action_draw(rng.seed, id, g));
         } else {
-            a = greedy_action<N>(s, eng);
+            a = policy_action<N, POLICY>(s, eng);
         }
         if (openings && rl > 0) s.meta -= 1u << M_RAND_SHIFT;
         step_lane<N>(s, a, flags, r, d, win, eng);
@@ -750,16 +791,16 @@ __global__ __launch_bounds__(BLOCK) void k_legal_moves(const uint64_t* __restric
     for (int i = 0; i < W; ++i) out[(size_t)e * W + i] = L.w[i];
 }
 
-template <int N>
-__global__ __launch_bounds__(BLOCK) void k_greedy(const uint64_t* __restrict__ boards,
-                                                  const uint16_t* __restrict__ meta,
-                                                  const uint64_t* __restrict__ legal, int E,
-                                                  int32_t* __restrict__ out) {
+template <int N, int POLICY>
+__global__ __launch_bounds__(BLOCK) void k_policy_actions(const uint64_t* __restrict__ boards,
+                                                          const uint16_t* __restrict__ meta,
+                                                          const uint64_t* __restrict__ legal, int E,
+                                                          int32_t* __restrict__ out) {
     const int e = blockIdx.x * BLOCK + threadIdx.x;
     if (e >= E) return;
     Lane<N> s;
     load_lane<N>(s, boards, meta, legal, e);
-    out[e] = greedy_action<N>(s, Solo<N>(0, nullptr));
+    out[e] = policy_action<N, POLICY>(s, Solo<N>(0, nullptr));
 }
 
 template <int N>
@@ -856,392 +897,4 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const uint64_t* __restrict__ 
     }
 }
 
-// ------------------------------------------------------------------------
-// host side
-// ------------------------------------------------------------------------
-thread_local std::string g_last_error;
-
-int fail(int code, const char* msg) {
-    g_last_error = msg;
-    return code;
-}
-
-int hip_fail(hipError_t err, const char* where) {
-    char buf[256];
-    snprintf(buf, sizeof(buf), "%s: %s", where, hipGetErrorString(err));
-    g_last_error = buf;
-    return OTH_EHIP;
-}
-
-#define OTH_HIP(call)                                       \
-    do {                                                    \
-        hipError_t err_ = (call);                           \
-        if (err_ != hipSuccess) return hip_fail(err_, #call); \
-    } while (0)
-
-int after_launch(const char* what) {
-    hipError_t err = hipGetLastError();
-    if (err != hipSuccess) return hip_fail(err, what);
-    return OTH_OK;
-}
-
-template <typename Fn>
-int with_n(int n, Fn&& fn) {
-    switch (n) {
-        case 4: return fn(std::integral_constant<int, 4>{});
-        case 5: return fn(std::integral_constant<int, 5>{});
-        case 6: return fn(std::integral_constant<int, 6>{});
-        case 7: return fn(std::integral_constant<int, 7>{});
-        case 8: return fn(std::integral_constant<int, 8>{});
-        case 9: return fn(std::integral_constant<int, 9>{});
-        case 10: return fn(std::integral_constant<int, 10>{});
-        case 11: return fn(std::integral_constant<int, 11>{});
-        case 12: return fn(std::integral_constant<int, 12>{});
-        case 13: return fn(std::integral_constant<int, 13>{});
-        case 14: return fn(std::integral_constant<int, 14>{});
-        case 15: return fn(std::integral_constant<int, 15>{});
-        case 16: return fn(std::integral_constant<int, 16>{});
-        default: return fail(OTH_EINVAL, "board_size must be in [4, 16]");
-    }
-}
-
-int grid_for(long long work) { return (int)((work + BLOCK - 1) / BLOCK); }
-
-}  // namespace
-
-struct oth_env {
-    int32_t E;
-    int32_t n;
-    int32_t W;
-    uint32_t flags;
-    uint64_t seed;
-    uint32_t id_base;
-    int32_t init_rand;
-    int32_t device;
-    uint64_t ply;
-    uint64_t* boards;
-    uint16_t* meta;
-    uint64_t* legal;
-    unsigned long long* wdl;  // [nslots][4] per-block W/D/L slots (tally)
-    int32_t nslots;
-};
-
-namespace {
-int use_device(const oth_env* env) {
-    int cur = -1;
-    OTH_HIP(hipGetDevice(&cur));
-    if (cur != env->device) OTH_HIP(hipSetDevice(env->device));
-    return OTH_OK;
-}
-
-#define OTH_CHECK_ENV(env)                                                  \
-    do {                                                                    \
-        if (!(env)) return fail(OTH_EINVAL, "NULL oth_env");               \
-        int rc_ = use_device(env);                                          \
-        if (rc_) return rc_;                                                \
-    } while (0)
-
-Rng rng_of(const oth_env* env) { return Rng{env->seed, env->id_base, env->init_rand}; }
-}  // namespace
-
-extern "C" {
-
-const char* oth_last_error(void) { return g_last_error.c_str(); }
-
-const char* oth_version(void) { return "othello_mi355x 0.1 (gfx950)"; }
-
-int oth_create(int32_t n_envs, int32_t board_size, uint32_t flags, uint64_t seed, uint32_t env_id_base,
-               int32_t initial_rand_steps, int32_t device, oth_env** out) {
-    if (!out) return fail(OTH_EINVAL, "out is NULL");
-    *out = nullptr;
-    if (n_envs <= 0) return fail(OTH_EINVAL, "n_envs must be > 0");
-    const int n = board_size < 4 ? 4 : board_size;  // othello.py:230
-    if (n > 16) return fail(OTH_EINVAL, "board_size must be <= 16");
-    if (initial_rand_steps < 0 || initial_rand_steps > 255)
-        return fail(OTH_EINVAL, "initial_rand_steps must be in [0, 255]");
-    if (flags & ~7u) return fail(OTH_EINVAL, "unknown flag bits");
-    OTH_HIP(hipSetDevice(device));
-    oth_env* env = new (std::nothrow) oth_env();
-    if (!env) return fail(OTH_ENOMEM, "host allocation failed");
-    env->E = n_envs;
-    env->n = n;
-    env->W = (n * n + 63) / 64;
-    env->flags = flags;
-    env->seed = seed;
-    env->id_base = env_id_base;
-    env->init_rand = initial_rand_steps;
-    env->device = device;
-    env->ply = 0;
-    const size_t E = (size_t)n_envs, W = (size_t)env->W;
-    hipError_t err = hipMalloc((void**)&env->boards, E * 2 * W * sizeof(uint64_t));
-    if (err == hipSuccess) err = hipMalloc((void**)&env->meta, ((E * sizeof(uint16_t) + 15) / 16) * 16);
-    if (err == hipSuccess) err = hipMalloc((void**)&env->legal, E * W * sizeof(uint64_t));
-    env->nslots = (int32_t)((2 * E + BLOCK - 1) / BLOCK);  // the widest grid (Pair: 2 lanes per board)
-    const size_t slot_bytes = (size_t)env->nslots * 4 * sizeof(unsigned long long);
-    if (err == hipSuccess) err = hipMalloc((void**)&env->wdl, slot_bytes);
-    if (err == hipSuccess) err = hipMemset(env->wdl, 0, slot_bytes);
-    if (err != hipSuccess) {
-        oth_destroy(env);
-        return hip_fail(err, "oth_create: allocation");
-    }
-    int rc = oth_reset(env, nullptr, nullptr);
-    if (rc == OTH_OK) {
-        err = hipStreamSynchronize(nullptr);
-        if (err != hipSuccess) rc = hip_fail(err, "oth_create: reset");
-    }
-    if (rc != OTH_OK) {
-        oth_destroy(env);
-        return rc;
-    }
-    *out = env;
-    return OTH_OK;
-}
-
-int oth_destroy(oth_env* env) {
-    if (!env) return OTH_OK;
-    (void)hipSetDevice(env->device);
-    if (env->boards) (void)hipFree(env->boards);
-    if (env->meta) (void)hipFree(env->meta);
-    if (env->legal) (void)hipFree(env->legal);
-    if (env->wdl) (void)hipFree(env->wdl);
-    delete env;
-    return OTH_OK;
-}
-
-int oth_reset(oth_env* env, const uint8_t* mask, oth_stream_t stream) {
-    OTH_CHECK_ENV(env);
-    return with_n(env->n, [&](auto NC) {
-        constexpr int N = decltype(NC)::value;
-        hipLaunchKernelGGL(k_reset<N>, dim3(grid_for(env->E)), dim3(BLOCK), 0, (hipStream_t)stream, env->boards,
-                           env->meta, env->legal, env->E, mask, rng_of(env), env->ply);
-        return after_launch("oth_reset");
-    });
-}
-
-int oth_step(oth_env* env, const int32_t* actions, int32_t* rewards, uint8_t* dones, oth_stream_t stream) {
-    OTH_CHECK_ENV(env);
-    if (!actions) return fail(OTH_EINVAL, "actions is NULL");
-    const uint64_t ply = env->ply++;
-    return with_n(env->n, [&](auto NC) {
-        constexpr int N = decltype(NC)::value;
-        hipLaunchKernelGGL(k_step<N>, dim3(grid_for(env->E)), dim3(BLOCK), 0, (hipStream_t)stream, env->boards,
-                           env->meta, env->legal, env->E, env->flags, actions, rewards, dones, env->wdl,
-                           rng_of(env), ply);
-        return after_launch("oth_step");
-    });
-}
-
-int oth_step_policy(oth_env* env, int32_t policy, int32_t n_plies, int32_t* actions, int32_t* rewards,
-                    uint8_t* dones, oth_stream_t stream) {
-    OTH_CHECK_ENV(env);
-    if (n_plies < 0) return fail(OTH_EINVAL, "n_plies must be >= 0");
-    if (policy != OTH_POLICY_RANDOM && policy != OTH_POLICY_GREEDY) return fail(OTH_EINVAL, "unknown policy");
-    if (n_plies == 0) return OTH_OK;
-    const uint64_t ply0 = env->ply;
-    env->ply += (uint64_t)n_plies;
-    return with_n(env->n, [&](auto NC) {
-        constexpr int N = decltype(NC)::value;
-        hipStream_t st = (hipStream_t)stream;
-        if constexpr (Geo<N>::W == 1 && OTH_PAIR) {
-            const dim3 grid(grid_for(2ll * env->E));
-            if (policy == OTH_POLICY_RANDOM)
-                hipLaunchKernelGGL((k_play<N, OTH_POLICY_RANDOM, Pair<N>>), grid, dim3(BLOCK), 0, st, env->boards,
-                                   env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards, dones,
-                                   env->wdl, rng_of(env), ply0);
-            else
-                hipLaunchKernelGGL((k_play<N, OTH_POLICY_GREEDY, Pair<N>>), grid, dim3(BLOCK), 0, st, env->boards,
-                                   env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards, dones,
-                                   env->wdl, rng_of(env), ply0);
-        } else if constexpr (Geo<N>::W == 1 && OTH_RAYS) {
-            // random play: ray-table flips; greedy: Kogge-Stone flips in the
-            // candidate loop (the ray tables' exposed LDS latency measured -10 %)
-            const dim3 grid(grid_for(env->E));
-            if (policy == OTH_POLICY_RANDOM)
-                hipLaunchKernelGGL((k_play<N, OTH_POLICY_RANDOM, Rays<N>>), grid, dim3(BLOCK), 0, st, env->boards,
-                                   env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards, dones,
-                                   env->wdl, rng_of(env), ply0);
-            else
-                hipLaunchKernelGGL((k_play<N, OTH_POLICY_GREEDY, Solo<N>>), grid, dim3(BLOCK), 0, st, env->boards,
-                                   env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards, dones,
-                                   env->wdl, rng_of(env), ply0);
-        } else {
-            const dim3 grid(grid_for(env->E));
-            if (policy == OTH_POLICY_RANDOM)
-                hipLaunchKernelGGL((k_play<N, OTH_POLICY_RANDOM, Solo<N>>), grid, dim3(BLOCK), 0, st, env->boards,
-                                   env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards, dones,
-                                   env->wdl, rng_of(env), ply0);
-            else
-                hipLaunchKernelGGL((k_play<N, OTH_POLICY_GREEDY, Solo<N>>), grid, dim3(BLOCK), 0, st, env->boards,
-                                   env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards, dones,
-                                   env->wdl, rng_of(env), ply0);
-        }
-        return after_launch("oth_step_policy");
-    });
-}
-
-int oth_reset_vs(oth_env* env, int32_t opponent_policy, const int8_t* protagonist, const uint8_t* mask,
-                 oth_stream_t stream) {
-    OTH_CHECK_ENV(env);
-    if (opponent_policy != OTH_POLICY_RANDOM && opponent_policy != OTH_POLICY_GREEDY)
-        return fail(OTH_EINVAL, "unknown opponent policy");
-    const uint64_t call = env->ply++;
-    return with_n(env->n, [&](auto NC) {
-        constexpr int N = decltype(NC)::value;
-        hipStream_t st = (hipStream_t)stream;
-        if (opponent_policy == OTH_POLICY_RANDOM)
-            hipLaunchKernelGGL((k_reset_vs<N, OTH_POLICY_RANDOM>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st,
-                               env->boards, env->meta, env->legal, env->E, env->flags, protagonist, mask,
-                               rng_of(env), call);
-        else
-            hipLaunchKernelGGL((k_reset_vs<N, OTH_POLICY_GREEDY>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st,
-                               env->boards, env->meta, env->legal, env->E, env->flags, protagonist, mask,
-                               rng_of(env), call);
-        return after_launch("oth_reset_vs");
-    });
-}
-
-int oth_step_vs(oth_env* env, int32_t opponent_policy, const int32_t* actions, const int8_t* protagonist,
-                int32_t* rewards, uint8_t* dones, int32_t* plies, oth_stream_t stream) {
-    OTH_CHECK_ENV(env);
-    if (!actions) return fail(OTH_EINVAL, "actions is NULL");
-    if (opponent_policy != OTH_POLICY_RANDOM && opponent_policy != OTH_POLICY_GREEDY)
-        return fail(OTH_EINVAL, "unknown opponent policy");
-    const uint64_t call = env->ply++;
-    return with_n(env->n, [&](auto NC) {
-        constexpr int N = decltype(NC)::value;
-        hipStream_t st = (hipStream_t)stream;
-        if (opponent_policy == OTH_POLICY_RANDOM)
-            hipLaunchKernelGGL((k_step_vs<N, OTH_POLICY_RANDOM>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st,
-                               env->boards, env->meta, env->legal, env->E, env->flags, actions, protagonist,
-                               rewards, dones, plies, env->wdl, rng_of(env), call);
-        else
-            hipLaunchKernelGGL((k_step_vs<N, OTH_POLICY_GREEDY>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st,
-                               env->boards, env->meta, env->legal, env->E, env->flags, actions, protagonist,
-                               rewards, dones, plies, env->wdl, rng_of(env), call);
-        return after_launch("oth_step_vs");
-    });
-}
-
-int oth_legal(oth_env* env, uint64_t* out, oth_stream_t stream) {
-    OTH_CHECK_ENV(env);
-    if (!out) return fail(OTH_EINVAL, "out is NULL");
-    OTH_HIP(hipMemcpyAsync(out, env->legal, (size_t)env->E * env->W * sizeof(uint64_t), hipMemcpyDeviceToDevice,
-                           (hipStream_t)stream));
-    return OTH_OK;
-}
-
-int oth_legal_moves(int32_t board_size, int32_t n, const uint64_t* mover, const uint64_t* opp, uint64_t* out,
-                    oth_stream_t stream) {
-    if (n < 0 || (n > 0 && (!mover || !opp || !out))) return fail(OTH_EINVAL, "bad arguments");
-    if (n == 0) return OTH_OK;
-    const int bs = board_size < 4 ? 4 : board_size;
-    return with_n(bs, [&](auto NC) {
-        constexpr int N = decltype(NC)::value;
-        hipLaunchKernelGGL(k_legal_moves<N>, dim3(grid_for(n)), dim3(BLOCK), 0, (hipStream_t)stream, mover, opp,
-                           out, n);
-        return after_launch("oth_legal_moves");
-    });
-}
-
-int oth_greedy_actions(oth_env* env, int32_t* out, oth_stream_t stream) {
-    OTH_CHECK_ENV(env);
-    if (!out) return fail(OTH_EINVAL, "out is NULL");
-    return with_n(env->n, [&](auto NC) {
-        constexpr int N = decltype(NC)::value;
-        hipLaunchKernelGGL(k_greedy<N>, dim3(grid_for(env->E)), dim3(BLOCK), 0, (hipStream_t)stream, env->boards,
-                           env->meta, env->legal, env->E, out);
-        return after_launch("oth_greedy_actions");
-    });
-}
-
-int oth_observe(oth_env* env, int32_t layout, int32_t dtype, void* out, oth_stream_t stream) {
-    OTH_CHECK_ENV(env);
-    if (!out) return fail(OTH_EINVAL, "out is NULL");
-    if (layout < OTH_OBS_BOARD || layout > OTH_OBS_ABSOLUTE) return fail(OTH_EINVAL, "unknown layout");
-    if (dtype < OTH_I8 || dtype > OTH_F64) return fail(OTH_EINVAL, "unknown dtype");
-    const int planes = layout == OTH_OBS_BOARD_LEGAL ? 2 : (layout == OTH_OBS_MAKE_STATE ? 4 : 1);
-    const long long total = (long long)env->E * planes * env->n * env->n;
-    int grid = grid_for(total);
-    if (grid > 65536) grid = 65536;
-    return with_n(env->n, [&](auto NC) {
-        constexpr int N = decltype(NC)::value;
-        hipLaunchKernelGGL(k_observe<N>, dim3(grid), dim3(BLOCK), 0, (hipStream_t)stream, env->boards, env->meta,
-                           env->legal, env->E, layout, dtype, out);
-        return after_launch("oth_observe");
-    });
-}
-
-int oth_get_state(oth_env* env, uint64_t* boards, uint16_t* meta, uint64_t* legal, oth_stream_t stream) {
-    OTH_CHECK_ENV(env);
-    const size_t E = (size_t)env->E, W = (size_t)env->W;
-    hipStream_t s = (hipStream_t)stream;
-    if (boards) OTH_HIP(hipMemcpyAsync(boards, env->boards, E * 2 * W * 8, hipMemcpyDefault, s));
-    if (meta) OTH_HIP(hipMemcpyAsync(meta, env->meta, E * 2, hipMemcpyDefault, s));
-    if (legal) OTH_HIP(hipMemcpyAsync(legal, env->legal, E * W * 8, hipMemcpyDefault, s));
-    return OTH_OK;
-}
-
-int oth_set_state(oth_env* env, const uint64_t* boards, const uint16_t* meta, const uint64_t* legal,
-                  oth_stream_t stream) {
-    OTH_CHECK_ENV(env);
-    const size_t E = (size_t)env->E, W = (size_t)env->W;
-    hipStream_t s = (hipStream_t)stream;
-    if (boards) OTH_HIP(hipMemcpyAsync(env->boards, boards, E * 2 * W * 8, hipMemcpyDefault, s));
-    if (meta) OTH_HIP(hipMemcpyAsync(env->meta, meta, E * 2, hipMemcpyDefault, s));
-    if (legal) OTH_HIP(hipMemcpyAsync(env->legal, legal, E * W * 8, hipMemcpyDefault, s));
-    return OTH_OK;
-}
-
-int oth_set_player_turn(oth_env* env, int32_t turn, const uint8_t* mask, oth_stream_t stream) {
-    OTH_CHECK_ENV(env);
-    if (turn != WHITE_DISK && turn != BLACK_DISK) return fail(OTH_EINVAL, "turn must be +1 or -1");
-    return with_n(env->n, [&](auto NC) {
-        constexpr int N = decltype(NC)::value;
-        hipLaunchKernelGGL(k_set_turn<N>, dim3(grid_for(env->E)), dim3(BLOCK), 0, (hipStream_t)stream,
-                           env->boards, env->meta, env->legal, env->E, turn, mask);
-        return after_launch("oth_set_player_turn");
-    });
-}
-
-int oth_count_disks(oth_env* env, int32_t* out, oth_stream_t stream) {
-    OTH_CHECK_ENV(env);
-    if (!out) return fail(OTH_EINVAL, "out is NULL");
-    return with_n(env->n, [&](auto NC) {
-        constexpr int N = decltype(NC)::value;
-        hipLaunchKernelGGL(k_count<N>, dim3(grid_for(env->E)), dim3(BLOCK), 0, (hipStream_t)stream, env->boards,
-                           env->E, out);
-        return after_launch("oth_count_disks");
-    });
-}
-
-int oth_counts(oth_env* env, int64_t* out, int32_t reset, oth_stream_t stream) {
-    OTH_CHECK_ENV(env);
-    if (!out) return fail(OTH_EINVAL, "out is NULL");
-    hipStream_t s = (hipStream_t)stream;
-#if OTH_TALLY_SLOTS
-    hipLaunchKernelGGL(k_reduce_wdl, dim3(1), dim3(256), 0, s, env->wdl, env->nslots, out, reset ? 1 : 0);
-    return after_launch("oth_counts");
-#else
-    OTH_HIP(hipMemcpyAsync(out, env->wdl, 3 * sizeof(int64_t), hipMemcpyDefault, s));
-    if (reset) OTH_HIP(hipMemsetAsync(env->wdl, 0, 4 * sizeof(unsigned long long), s));
-    return OTH_OK;
-#endif
-}
-
-uint64_t oth_ply_counter(const oth_env* env) { return env ? env->ply : 0; }
-
-int oth_set_ply_counter(oth_env* env, uint64_t ply) {
-    if (!env) return fail(OTH_EINVAL, "NULL oth_env");
-    env->ply = ply;
-    return OTH_OK;
-}
-
-int oth_shape(const oth_env* env, int32_t* n_envs, int32_t* board_size, int32_t* words) {
-    if (!env) return fail(OTH_EINVAL, "NULL oth_env");
-    if (n_envs) *n_envs = env->E;
-    if (board_size) *board_size = env->n;
-    if (words) *words = env->W;
-    return OTH_OK;
-}
-
-}  // extern "C"
+}  // namespace oth_dev

@@ -1,0 +1,154 @@
+// kernels_n.hip -- kernel launchers for ONE board size, compiled once per N
+// (-DOTH_N=4 .. 16) so the 13 template sets build in parallel.
+#include <type_traits>
+
+#include "device.hpp"
+#include "launch.hpp"
+
+#ifndef OTH_N
+#error "compile with -DOTH_N=<board size>"
+#endif
+
+using namespace oth;
+using namespace oth_dev;
+
+namespace oth_host {
+namespace {
+
+int grid_for(long long work) { return (int)((work + BLOCK - 1) / BLOCK); }
+
+Rng rng_of(const oth_env* env) { return Rng{env->seed, env->id_base, env->init_rand}; }
+
+// Compile-time policy for a runtime id (OTH_POLICY_*); MAXIMIN1 is GREEDY
+// (same move: simple_policies.py:111-155 at depth 1 is GreedyPolicy's argmax).
+template <typename Fn>
+int with_policy(int policy, Fn&& fn) {
+    switch (policy) {
+        case OTH_POLICY_RANDOM: return fn(std::integral_constant<int, OTH_POLICY_RANDOM>{});
+        case OTH_POLICY_GREEDY:
+        case OTH_POLICY_MAXIMIN1: return fn(std::integral_constant<int, OTH_POLICY_GREEDY>{});
+        case OTH_POLICY_MAXIMIN2: return fn(std::integral_constant<int, OTH_POLICY_MAXIMIN2>{});
+        case OTH_POLICY_MAXIMIN3: return fn(std::integral_constant<int, OTH_POLICY_MAXIMIN3>{});
+        default: return fail(OTH_EINVAL, "unknown policy");
+    }
+}
+
+}  // namespace
+
+template <int N>
+int launch_reset(oth_env* env, const uint8_t* mask, hipStream_t st) {
+    hipLaunchKernelGGL(k_reset<N>, dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards, env->meta, env->legal,
+                       env->E, mask, rng_of(env), env->ply);
+    return after_launch("oth_reset");
+}
+
+template <int N>
+int launch_step(oth_env* env, const int32_t* actions, int32_t* rewards, uint8_t* dones, uint64_t ply,
+                hipStream_t st) {
+    hipLaunchKernelGGL(k_step<N>, dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards, env->meta, env->legal,
+                       env->E, env->flags, actions, rewards, dones, env->wdl, rng_of(env), ply);
+    return after_launch("oth_step");
+}
+
+template <int N>
+int launch_play(oth_env* env, int policy, int n_plies, int32_t* actions, int32_t* rewards, uint8_t* dones,
+                uint64_t ply0, hipStream_t st) {
+    return with_policy(policy, [&](auto PC) {
+        constexpr int POL = decltype(PC)::value;
+        if constexpr (Geo<N>::W == 1 && OTH_PAIR && POL != OTH_POLICY_MAXIMIN2 && POL != OTH_POLICY_MAXIMIN3) {
+            hipLaunchKernelGGL((k_play<N, POL, Pair<N>>), dim3(grid_for(2ll * env->E)), dim3(BLOCK), 0, st,
+                               env->boards, env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards,
+                               dones, env->wdl, rng_of(env), ply0);
+        } else if constexpr (Geo<N>::W == 1 && OTH_RAYS && POL == OTH_POLICY_RANDOM) {
+            // random play: ray-table flips; the scripted policies keep Kogge-Stone
+            // flips in their candidate loops (the ray tables' exposed LDS latency
+            // measured -10 % for greedy)
+            hipLaunchKernelGGL((k_play<N, POL, Rays<N>>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards,
+                               env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards, dones, env->wdl,
+                               rng_of(env), ply0);
+        } else {
+            hipLaunchKernelGGL((k_play<N, POL, Solo<N>>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards,
+                               env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards, dones, env->wdl,
+                               rng_of(env), ply0);
+        }
+        return after_launch("oth_step_policy");
+    });
+}
+
+template <int N>
+int launch_reset_vs(oth_env* env, int policy, const int8_t* prot, const uint8_t* mask, uint64_t call,
+                    hipStream_t st) {
+    return with_policy(policy, [&](auto PC) {
+        constexpr int POL = decltype(PC)::value;
+        hipLaunchKernelGGL((k_reset_vs<N, POL>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards, env->meta,
+                           env->legal, env->E, env->flags, prot, mask, rng_of(env), call);
+        return after_launch("oth_reset_vs");
+    });
+}
+
+template <int N>
+int launch_step_vs(oth_env* env, int policy, const int32_t* actions, const int8_t* prot, int32_t* rewards,
+                   uint8_t* dones, int32_t* plies, uint64_t call, hipStream_t st) {
+    return with_policy(policy, [&](auto PC) {
+        constexpr int POL = decltype(PC)::value;
+        hipLaunchKernelGGL((k_step_vs<N, POL>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards, env->meta,
+                           env->legal, env->E, env->flags, actions, prot, rewards, dones, plies, env->wdl,
+                           rng_of(env), call);
+        return after_launch("oth_step_vs");
+    });
+}
+
+template <int N>
+int launch_policy_actions(oth_env* env, int policy, int32_t* out, hipStream_t st) {
+    return with_policy(policy, [&](auto PC) {
+        constexpr int POL = decltype(PC)::value;
+        if constexpr (POL != OTH_POLICY_RANDOM)
+            hipLaunchKernelGGL((k_policy_actions<N, POL>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards,
+                               env->meta, env->legal, env->E, out);
+        return after_launch("oth_policy_actions");
+    });
+}
+
+template <int N>
+int launch_legal_moves(int n, const uint64_t* mover, const uint64_t* opp, uint64_t* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_legal_moves<N>, dim3(grid_for(n)), dim3(BLOCK), 0, st, mover, opp, out, n);
+    return after_launch("oth_legal_moves");
+}
+
+template <int N>
+int launch_observe(oth_env* env, int layout, int dtype, void* out, hipStream_t st) {
+    const int planes = layout == OTH_OBS_BOARD_LEGAL ? 2 : (layout == OTH_OBS_MAKE_STATE ? 4 : 1);
+    const long long total = (long long)env->E * planes * N * N;
+    int grid = grid_for(total);
+    if (grid > 65536) grid = 65536;
+    hipLaunchKernelGGL(k_observe<N>, dim3(grid), dim3(BLOCK), 0, st, env->boards, env->meta, env->legal, env->E,
+                       layout, dtype, out);
+    return after_launch("oth_observe");
+}
+
+template <int N>
+int launch_set_turn(oth_env* env, int turn, const uint8_t* mask, hipStream_t st) {
+    hipLaunchKernelGGL(k_set_turn<N>, dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards, env->meta, env->legal,
+                       env->E, turn, mask);
+    return after_launch("oth_set_player_turn");
+}
+
+template <int N>
+int launch_count(oth_env* env, int32_t* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_count<N>, dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards, env->E, out);
+    return after_launch("oth_count_disks");
+}
+
+template int launch_reset<OTH_N>(oth_env*, const uint8_t*, hipStream_t);
+template int launch_step<OTH_N>(oth_env*, const int32_t*, int32_t*, uint8_t*, uint64_t, hipStream_t);
+template int launch_play<OTH_N>(oth_env*, int, int, int32_t*, int32_t*, uint8_t*, uint64_t, hipStream_t);
+template int launch_reset_vs<OTH_N>(oth_env*, int, const int8_t*, const uint8_t*, uint64_t, hipStream_t);
+template int launch_step_vs<OTH_N>(oth_env*, int, const int32_t*, const int8_t*, int32_t*, uint8_t*, int32_t*,
+                                   uint64_t, hipStream_t);
+template int launch_policy_actions<OTH_N>(oth_env*, int, int32_t*, hipStream_t);
+template int launch_legal_moves<OTH_N>(int, const uint64_t*, const uint64_t*, uint64_t*, hipStream_t);
+template int launch_observe<OTH_N>(oth_env*, int, int, void*, hipStream_t);
+template int launch_set_turn<OTH_N>(oth_env*, int, const uint8_t*, hipStream_t);
+template int launch_count<OTH_N>(oth_env*, int32_t*, hipStream_t);
+
+}  // namespace oth_host

@@ -1,0 +1,55 @@
+// launch.hpp -- host side shared by capi.hip and the per-board-size kernel
+// translation units (kernels_n.hip): the handle layout, error reporting, and
+// the launcher templates, one explicit instantiation per N in kernels_n.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "othello_mi355x.h"
+
+struct oth_env {
+    int32_t E;
+    int32_t n;
+    int32_t W;
+    uint32_t flags;
+    uint64_t seed;
+    uint32_t id_base;
+    int32_t init_rand;
+    int32_t device;
+    uint64_t ply;
+    uint64_t* boards;
+    uint16_t* meta;
+    uint64_t* legal;
+    unsigned long long* wdl;  // [nslots][4] per-block W/D/L slots (tally)
+    int32_t nslots;
+};
+
+namespace oth_host {
+
+// error reporting (capi.hip): set the thread's oth_last_error() and return the code
+int fail(int code, const char* msg);
+int hip_fail(hipError_t err, const char* where);
+int after_launch(const char* what);
+
+// one set per board size N (kernels_n.hip instantiates them)
+template <int N> int launch_reset(oth_env* env, const uint8_t* mask, hipStream_t st);
+template <int N>
+int launch_step(oth_env* env, const int32_t* actions, int32_t* rewards, uint8_t* dones, uint64_t ply,
+                hipStream_t st);
+template <int N>
+int launch_play(oth_env* env, int policy, int n_plies, int32_t* actions, int32_t* rewards, uint8_t* dones,
+                uint64_t ply0, hipStream_t st);
+template <int N>
+int launch_reset_vs(oth_env* env, int policy, const int8_t* prot, const uint8_t* mask, uint64_t call,
+                    hipStream_t st);
+template <int N>
+int launch_step_vs(oth_env* env, int policy, const int32_t* actions, const int8_t* prot, int32_t* rewards,
+                   uint8_t* dones, int32_t* plies, uint64_t call, hipStream_t st);
+template <int N> int launch_policy_actions(oth_env* env, int policy, int32_t* out, hipStream_t st);
+template <int N>
+int launch_legal_moves(int n, const uint64_t* mover, const uint64_t* opp, uint64_t* out, hipStream_t st);
+template <int N> int launch_observe(oth_env* env, int layout, int dtype, void* out, hipStream_t st);
+template <int N> int launch_set_turn(oth_env* env, int turn, const uint8_t* mask, hipStream_t st);
+template <int N> int launch_count(oth_env* env, int32_t* out, hipStream_t st);
+
+}  // namespace oth_host

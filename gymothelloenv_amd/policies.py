@@ -5,9 +5,11 @@
 
 RandomPolicy draws exactly like simple_policies.py:37-41 (np.random.RandomState
 index into possible_moves), so seeded games match the reference move for move.
-GreedyPolicy asks the device kernel (oth_greedy_actions) for the move of
-simple_policies.py:69-92 -- the one flipping the most discs, lowest square on
-ties -- instead of simulating every candidate on a copied env.
+GreedyPolicy and MaxiMinPolicy ask the device kernels (oth_policy_actions) for
+the move of simple_policies.py:69-92 / :98-163 -- greedy: the move flipping the
+most discs, lowest square on ties; maximin: the depth-limited max-min search
+with the reference's pass handling -- instead of simulating every candidate on
+copied envs.
 """
 import numpy as np
 
@@ -58,7 +60,7 @@ class GreedyPolicy(object):
             assert int((self.env.player_turn + 1) / 2) == int(obs[2][0][0])
         vec = self.env._vec
         self.env._sync()
-        a = int(vec.greedy_actions().cpu()[0])
+        a = int(vec.policy_actions("greedy").cpu()[0])
         if a < 0:
             raise ValueError('no possible moves')
         return a
@@ -67,4 +69,28 @@ class GreedyPolicy(object):
         return self.get_action(obs)
 
 
-__all__ = ['RandomPolicy', 'GreedyPolicy', 'PROTAGONIST_TURN', 'OPPONENT_TURN', 'WHITE_DISK']
+class MaxiMinPolicy(object):
+    """simple_policies.py:98-163 (max_search_depth 1..3), searched on the device."""
+
+    def __init__(self, max_search_depth=1):
+        if not 1 <= int(max_search_depth) <= 3:
+            raise ValueError("max_search_depth must be 1, 2 or 3 on the device")
+        self.env = None
+        self.max_search_depth = int(max_search_depth)
+
+    def reset(self, env):
+        self.env = _base(env)
+
+    def get_action(self, obs):
+        vec = self.env._vec
+        self.env._sync()
+        a = int(vec.policy_actions("maximin%d" % self.max_search_depth).cpu()[0])
+        if a < 0:
+            raise ValueError('no possible moves')
+        return a
+
+    def get_test_action(self, obs):
+        return self.get_action(obs)
+
+
+__all__ = ['RandomPolicy', 'GreedyPolicy', 'MaxiMinPolicy', 'PROTAGONIST_TURN', 'OPPONENT_TURN', 'WHITE_DISK']

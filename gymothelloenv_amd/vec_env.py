@@ -18,7 +18,9 @@ _OBS_LAYOUTS = {"board": L.OTH_OBS_BOARD, "board_legal": L.OTH_OBS_BOARD_LEGAL,
 _OBS_PLANES = {L.OTH_OBS_BOARD: 1, L.OTH_OBS_BOARD_LEGAL: 2, L.OTH_OBS_MAKE_STATE: 4, L.OTH_OBS_ABSOLUTE: 1}
 _DTYPES = {torch.int8: L.OTH_I8, torch.int32: L.OTH_I32, torch.int64: L.OTH_I64,
            torch.float32: L.OTH_F32, torch.float64: L.OTH_F64}
-_POLICIES = {"random": L.OTH_POLICY_RANDOM, "greedy": L.OTH_POLICY_GREEDY}
+_POLICIES = {"random": L.OTH_POLICY_RANDOM, "greedy": L.OTH_POLICY_GREEDY,
+             "maximin1": L.OTH_POLICY_MAXIMIN1, "maximin2": L.OTH_POLICY_MAXIMIN2,
+             "maximin3": L.OTH_POLICY_MAXIMIN3}
 
 BLACK_DISK, NO_DISK, WHITE_DISK = -1, 0, 1  # othello.py:10-12
 
@@ -122,7 +124,8 @@ class VecOthelloEnv(object):
 
     def step_policy(self, policy="random", n_plies=1, actions=None, rewards=None, dones=None, record=True):
         """n_plies plies where every board's mover plays `policy` on the device
-        (RandomPolicy simple_policies.py:37-41 / GreedyPolicy :69-92).
+        (RandomPolicy simple_policies.py:37-41, GreedyPolicy :69-92, MaxiMinPolicy
+        :98-163 as 'maximin1'..'maximin3').
 
         Returns (actions, rewards, dones) of shape (n_plies, E) (None if not recorded)."""
         pol = _POLICIES[policy] if isinstance(policy, str) else int(policy)
@@ -181,8 +184,15 @@ class VecOthelloEnv(object):
         return o[:, 1].reshape(self.num_envs, -1).bool()
 
     def greedy_actions(self):
+        """GreedyPolicy.get_action (simple_policies.py:69-92) for every board."""
+        return self.policy_actions("greedy")
+
+    def policy_actions(self, policy="greedy"):
+        """The move of a scripted policy ('greedy', 'maximin1'..'maximin3';
+        simple_policies.py:57-163) for the side to move on every board."""
         out = self._i32(self.num_envs)
-        L.check(self._lib.oth_greedy_actions(self._h, _ptr(out), self._stream()), "oth_greedy_actions")
+        L.check(self._lib.oth_policy_actions(self._h, _POLICIES[policy], _ptr(out), self._stream()),
+                "oth_policy_actions")
         return out
 
     def observe(self, layout="board", dtype=torch.int64, out=None):

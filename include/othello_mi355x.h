@@ -54,7 +54,15 @@ enum {
     OTH_AUTO_RESET = 4    /* batched only: reset an env right after its terminal ply */
 };
 
-enum { OTH_POLICY_RANDOM = 0, OTH_POLICY_GREEDY = 1 };
+/* on-device scripted policies (simple_policies.py): RandomPolicy, GreedyPolicy,
+ * MaxiMinPolicy(max_search_depth = 1, 2, 3); MAXIMIN1 plays exactly GREEDY's moves */
+enum {
+    OTH_POLICY_RANDOM = 0,
+    OTH_POLICY_GREEDY = 1,
+    OTH_POLICY_MAXIMIN1 = 2,
+    OTH_POLICY_MAXIMIN2 = 3,
+    OTH_POLICY_MAXIMIN3 = 4
+};
 
 /* observation layouts */
 enum {
@@ -127,6 +135,11 @@ int oth_legal_moves(int32_t board_size, int32_t n, const uint64_t *mover, const 
  * every env: argmax over possible_moves of the discs flipped, lowest square
  * on ties; -1 where possible_moves is empty.  Out int32[E]. */
 int oth_greedy_actions(oth_env *env, int32_t *out, oth_stream_t stream);
+
+/* The move of a deterministic scripted policy (OTH_POLICY_GREEDY or
+ * OTH_POLICY_MAXIMIN1..3: MaxiMinPolicy.get_action, simple_policies.py:157-163)
+ * for the side to move in every env; -1 where possible_moves is empty. */
+int oth_policy_actions(oth_env *env, int32_t policy, int32_t *out, oth_stream_t stream);
 
 /* Observations: layout OTH_OBS_*, dtype OTH_I8..OTH_F64, out (E, planes, N, N). */
 int oth_observe(oth_env *env, int32_t layout, int32_t dtype, void *out, oth_stream_t stream);

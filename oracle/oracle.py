@@ -44,6 +44,7 @@ def lib():
         L.oracle_greedy_batch.argtypes = [i32, i32, P, P, P, P]
         L.oracle_recompute_legal.argtypes = [i32, i32, P, P, P]
         L.oracle_observe.argtypes = [i32, i32, P, P, P, P, P, P]
+        L.oracle_maximin_batch.argtypes = [i32, i32, i32, P, P, P, P]
         L.oracle_reset_vs.argtypes = [i32, u32, i32, i32, u64, u32, u64, i32, P, P, P, P]
         L.oracle_step_vs.argtypes = [i32, u32, i32, i32, u64, u32, u64, i32, P, P, P, P, P, P, P, P, P]
         _lib = L
@@ -125,6 +126,13 @@ def rollout(s, flags, policy, plies, seed=0, id_base=0, ply0=0, initial_rand_ste
 def greedy(s):
     out = np.zeros(s.E, dtype=np.int32)
     lib().oracle_greedy_batch(s.n, s.E, _p(s.boards), _p(s.meta), _p(s.legal), _p(out))
+    return out
+
+
+def maximin(s, depth):
+    """MaxiMinPolicy(depth).get_action for every position of State s."""
+    out = np.zeros(s.E, dtype=np.int32)
+    lib().oracle_maximin_batch(s.n, depth, s.E, _p(s.boards), _p(s.meta), _p(s.legal), _p(out))
     return out
 
 

@@ -218,6 +218,16 @@ static int greedy_action(const oenv *e) {
     return best;
 }
 
+static int maximin_search(const oenv *e, int depth, int max_depth, int perspective, int my, int *move);
+
+/* the move of a deterministic scripted policy: 1 GreedyPolicy, 2..4 MaxiMinPolicy(1..3) */
+static int policy_move(const oenv *e, int policy) {
+    int mv;
+    if (policy == 1) return greedy_action(e);
+    maximin_search(e, 0, policy - 1, e->turn, e->turn, &mv);
+    return mv;
+}
+
 /* ---------------- Philox4x32-10 (the device RNG's specification) ---------------- */
 static void philox(uint32_t key0, uint32_t key1, uint32_t c[4]) {
     for (int r = 0; r < 10; r++) {
@@ -378,7 +388,7 @@ void oracle_reset_openings(int n, int E, uint64_t seed, uint32_t id_base, uint64
 }
 
 /* On-device-policy rollout semantics (oth_step_policy): `plies` plies over E
- * envs.  policy 0 = random, 1 = greedy.  Global ply index g = ply0 + p.
+ * envs.  policy 0 = random, 1 = greedy, 2..4 = maximin depth 1..3.  Global ply index g = ply0 + p.
  * actions/rewards/dones are [plies][E] (NULL to skip); wdl[3] accumulates
  * {black wins, draws, white wins} over games that end in this call. */
 int oracle_rollout(int n, uint32_t flags, int policy, int initial_rand_steps, uint64_t seed, uint32_t id_base,
@@ -399,7 +409,7 @@ int oracle_rollout(int n, uint32_t flags, int policy, int initial_rand_steps, ui
                     a = random_action(&e, seed, id, g);
                     if (e.rand_left > 0) e.rand_left--;
                 } else {
-                    a = greedy_action(&e);
+                    a = policy_move(&e, policy);
                 }
                 env_step(&e, a, &r, &d);
                 if (d) {
@@ -485,7 +495,7 @@ static void opponent_reply(oenv *e, int prot, int openings, int policy, uint64_t
         if (policy == 0 || (openings && e->rand_left > 0))
             a = random_action(e, seed, id, g);
         else
-            a = greedy_action(e);
+            a = policy_move(e, policy);
         if (openings && e->rand_left > 0) e->rand_left--;
         env_step(e, a, r, d);
     }
@@ -558,5 +568,52 @@ void oracle_step_vs(int n, uint32_t flags, int policy, int initial_rand_steps, u
         if (rewards) rewards[i] = r;
         if (dones) dones[i] = (uint8_t)d;
         if (plies) plies[i] = np;
+    }
+}
+
+/* ---------------- MaxiMinPolicy (simple_policies.py:98-163) ---------------- */
+/* search() restated with the reference's simulation: for each legal move a
+ * fresh copy gets the board (set_board_state), the turn (set_player_turn), the
+ * move (step); if the opponent must pass, the turn is forced to the opponent
+ * anyway (set_player_turn(-perspective), :139-144), whose empty move list then
+ * ends the branch.  Leaves count the searching side's discs; ties keep the
+ * first move (np.argmax / np.argmin). */
+static int maximin_search(const oenv *e, int depth, int max_depth, int perspective, int my, int *move) {
+    if (e->terminated || depth >= max_depth || e->nmoves == 0) {
+        int w, b;
+        count_disks(e, &w, &b);
+        *move = -1;
+        return my == WHITE_DISK ? w : b;
+    }
+    int best = 0, best_move = -1, have = 0;
+    for (int i = 0; i < e->nmoves; i++) {
+        oenv c = *e; /* copy_env + reset + set_board_state(...) */
+        int r, d, mv;
+        c.terminated = 0;
+        c.winner = NO_DISK;
+        set_player_turn(&c, perspective);
+        env_step(&c, e->moves[i], &r, &d);
+        if (!c.terminated && c.turn == perspective) set_player_turn(&c, -perspective);
+        int cnt = maximin_search(&c, depth + 1, max_depth, -perspective, my, &mv);
+        if (!have || (perspective == my ? cnt > best : cnt < best)) {
+            best = cnt;
+            best_move = e->moves[i];
+            have = 1;
+        }
+    }
+    *move = best_move;
+    return best;
+}
+
+/* MaxiMinPolicy(depth).get_action for E positions (exchange format). */
+void oracle_maximin_batch(int n, int depth, int E, const uint64_t *boards, const uint16_t *meta,
+                          const uint64_t *legal, int32_t *out) {
+    int W = nwords(n);
+    oenv e;
+    for (int i = 0; i < E; i++) {
+        int mv;
+        load(&e, n, F_SUDDEN_DEATH, boards + (size_t)i * 2 * W, meta[i], legal + (size_t)i * W);
+        maximin_search(&e, 0, depth, e.turn, e.turn, &mv);
+        out[i] = mv;
     }
 }

@@ -385,6 +385,39 @@ def gen_vs(othello):
     np.savez_compressed(os.path.join(OUT, "vs_greedy.npz"), **out)
 
 
+def gen_maximin(othello, simple_policies):
+    """MaxiMinPolicy(depth).get_action (simple_policies.py:98-163) on positions
+    from random play, depth 1..3, N = 6 and 8."""
+    out = {}
+    for n, counts in ((6, {1: 120, 2: 80, 3: 40}), (8, {1: 120, 2: 60, 3: 25})):
+        for depth, positions in counts.items():
+            rnd = np.random.RandomState(31 * n + depth)
+            env = othello.OthelloBaseEnv(board_size=n, mute=True)
+            pol = simple_policies.MaxiMinPolicy(depth)
+            pol.reset(env)
+            blacks, whites, turns, acts = [], [], [], []
+            while len(acts) < positions:
+                env.reset()
+                done = False
+                while not done and len(acts) < positions:
+                    if rnd.rand() < 0.3:
+                        a = pol.get_action(env.get_observation())
+                        b, w, t, _ = snapshot(env, n)
+                        blacks.append(b)
+                        whites.append(w)
+                        turns.append(t)
+                        acts.append(int(a))
+                    pm = env.possible_moves
+                    _, _, done, _ = env.step(int(pm[rnd.randint(0, len(pm))]))
+            key = "N%d_d%d_" % (n, depth)
+            out[key + "black"] = np.array(blacks, dtype=np.uint64)
+            out[key + "white"] = np.array(whites, dtype=np.uint64)
+            out[key + "turn"] = np.array(turns, dtype=np.int8)
+            out[key + "action"] = np.array(acts, dtype=np.int32)
+            print("maximin N=%d depth=%d: %d positions" % (n, depth, len(acts)))
+    np.savez_compressed(os.path.join(OUT, "maximin.npz"), **out)
+
+
 def main():
     install_shims()
     import othello  # noqa: E402  (reference, read-only)
@@ -396,6 +429,7 @@ def main():
     gen_obs(othello, util)
     gen_wrappers(othello, simple_policies)
     gen_vs(othello)
+    gen_maximin(othello, simple_policies)
 
 
 if __name__ == "__main__":

@@ -153,3 +153,21 @@ def test_greedy_policy_and_make_state(pkg, golden_dir, n):
         st = pkg.make_state(env.get_observation(), env)
         np.testing.assert_array_equal(st, o["N%d_make_state" % n][i].astype(np.float64))
         np.testing.assert_array_equal(pkg.undo_state(st, env.player_turn), env.get_observation())
+
+
+def test_maximin_policy_dropin(pkg, golden_dir):
+    g = np.load(os.path.join(golden_dir, "maximin.npz"))
+    env = pkg.OthelloBaseEnv(board_size=8, mute=True)
+    env.reset()
+    for depth in (1, 2, 3):
+        pol = pkg.MaxiMinPolicy(depth)
+        pol.reset(env)
+        k = "N8_d%d_" % depth
+        for i in range(0, len(g[k + "action"]), 5):
+            bl, wh = g[k + "black"][i], g[k + "white"][i]
+            board = np.zeros(64, dtype=np.int64)
+            for a in range(64):
+                board[a] = -1 if (int(bl[0]) >> a) & 1 else (1 if (int(wh[0]) >> a) & 1 else 0)
+            env.set_board_state(board.reshape(8, 8), perspective=1)
+            env.set_player_turn(int(g[k + "turn"][i]))
+            assert pol.get_action(env.get_observation()) == int(g[k + "action"][i])

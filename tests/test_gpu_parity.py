@@ -361,3 +361,56 @@ def test_vs_rollout_replays_on_oracle(torch_cuda, n, opp, init_rand):
     np.testing.assert_array_equal(m, s.meta)
     np.testing.assert_array_equal(lg, s.legal)
     np.testing.assert_array_equal(env.counts().cpu().numpy(), wdl)
+
+
+@pytest.mark.parametrize("n,depth", [(6, 1), (6, 2), (6, 3), (8, 1), (8, 2), (8, 3)])
+def test_maximin_actions_match_reference(torch_cuda, golden_dir, n, depth):
+    """MaxiMinPolicy(depth).get_action (simple_policies.py:98-163) on device."""
+    torch = torch_cuda
+    g = np.load(os.path.join(golden_dir, "maximin.npz"))
+    k = "N%d_d%d_" % (n, depth)
+    b, w, t, a = g[k + "black"], g[k + "white"], g[k + "turn"], g[k + "action"]
+    env = make_env(torch, len(a), n)
+    env.set_state(t64(torch, np.concatenate([b, w], axis=1)),
+                  torch.from_numpy(oracle.meta_from(t).view(np.int16)).cuda())
+    env.set_player_turn(1, mask=torch.from_numpy((t == 1).astype(np.uint8)).cuda())
+    env.set_player_turn(-1, mask=torch.from_numpy((t == -1).astype(np.uint8)).cuda())
+    np.testing.assert_array_equal(env.policy_actions("maximin%d" % depth).cpu().numpy(), a)
+
+
+@pytest.mark.parametrize("n,policy,pid", [(8, "maximin2", 3), (6, "maximin3", 4), (10, "maximin2", 3)])
+def test_maximin_rollout_replays_on_oracle(torch_cuda, n, policy, pid):
+    torch = torch_cuda
+    E, plies = 512, 70
+    env = make_env(torch, E, n, auto=True, seed=23, init_rand=8)
+    env.reset()
+    acts, rews, dones = env.step_policy(policy, n_plies=plies)
+    b, m, lg = get_state_np(env)
+    s = oracle.reset_openings(n, E, 23, 0, 0, 8)
+    oa, orw, od, owdl = oracle.rollout(s, flags_of(True, False, True), pid, plies, seed=23, initial_rand_steps=8)
+    np.testing.assert_array_equal(acts.cpu().numpy(), oa)
+    np.testing.assert_array_equal(rews.cpu().numpy(), orw)
+    np.testing.assert_array_equal(dones.cpu().numpy(), od)
+    np.testing.assert_array_equal(b, s.boards)
+    np.testing.assert_array_equal(env.counts().cpu().numpy(), owdl)
+
+
+def test_vs_maximin_opponent_on_oracle(torch_cuda):
+    torch = torch_cuda
+    n, E, calls = 8, 1024, 40
+    prot = np.where(np.arange(E) % 2 == 0, -1, 1).astype(np.int8)
+    env = make_env(torch, E, n, auto=True, seed=29, init_rand=4)
+    env.reset_vs("maximin2", protagonist=torch.from_numpy(prot))
+    s = oracle.reset_vs(n, E, flags_of(True, False, True), 3, 0, seed=29, initial_rand_steps=4, prot=prot)
+    rng = np.random.RandomState(1)
+    for c in range(1, calls + 1):
+        lb = legal_bool(s.legal, n)
+        acts = np.argmax(rng.rand(E, n * n) * lb, axis=1).astype(np.int32)
+        orw, od, opl = oracle.step_vs(s, flags_of(True, False, True), 3, c, acts, seed=29, initial_rand_steps=4,
+                                      prot=prot)
+        _, rew, dn, plies = env.step_vs(torch.from_numpy(acts).cuda(), "maximin2", observe=False)
+        np.testing.assert_array_equal(rew.cpu().numpy(), orw)
+        np.testing.assert_array_equal(dn.cpu().numpy(), od.astype(bool))
+        np.testing.assert_array_equal(plies.cpu().numpy(), opl)
+    b, m, lg = get_state_np(env)
+    np.testing.assert_array_equal(b, s.boards)

@@ -176,3 +176,17 @@ def test_vs_greedy_matches_reference(golden_dir, n):
                 assert list(s.boards[0]) == list(v["N%d_black" % n][i]) + list(v["N%d_white" % n][i])
                 assert (1 if s.meta[0] & 1 else -1) == v["N%d_turn" % n][i]
                 assert plies[0] >= 1
+
+
+@pytest.mark.parametrize("n,depth", [(6, 1), (6, 2), (6, 3), (8, 1), (8, 2), (8, 3)])
+def test_maximin_matches_reference(golden_dir, n, depth):
+    g = np.load(os.path.join(golden_dir, "maximin.npz"))
+    k = "N%d_d%d_" % (n, depth)
+    b, w, t, a = g[k + "black"], g[k + "white"], g[k + "turn"], g[k + "action"]
+    s = oracle.State(n, len(a))
+    s.boards[:] = np.concatenate([b, w], axis=1)
+    s.meta[:] = oracle.meta_from(t)
+    s.legal[:] = oracle.recompute_legal(s)
+    np.testing.assert_array_equal(oracle.maximin(s, depth), a)
+    if depth == 1:  # MaxiMin-1 == Greedy (README.md:48: identical rows)
+        np.testing.assert_array_equal(oracle.greedy(s), a)

@@ -24,11 +24,7 @@ def build(specs):
     os.makedirs(VDIR, exist_ok=True)
     for spec in specs:
         name, _, flags = spec.partition("=")
-        out = os.path.join(VDIR, "liboth_%s.so" % name)
-        cmd = [hb.HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-I", os.path.join(ROOT, "include")] + flags.split() + ["-o", out] + hb.SRC
-        print(" ".join(cmd), flush=True)
-        subprocess.check_call(cmd)
+        hb.build(force=True, extra_flags=flags.split(), out=os.path.join(VDIR, "liboth_%s.so" % name))
 
 
 def run(names, E, n, plies, launches, rounds, policy, check=True):
