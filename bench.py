@@ -87,11 +87,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--envs", type=int, default=65536, help="boards per GPU")
     ap.add_argument("--board-size", type=int, default=8)
-    ap.add_argument("--policy", default="random", choices=["random", "greedy"])
+    ap.add_argument("--policy", default="random", choices=["random", "greedy", "maximin1", "maximin2", "maximin3"])
     ap.add_argument("--plies-per-launch", type=int, default=None)
     ap.add_argument("--no-record", action="store_true", help="do not store per-ply action/reward/done")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-single-ply", action="store_true", help="skip the one-ply-per-launch side measurement")
     args = ap.parse_args()
 
     import torch
@@ -156,6 +157,29 @@ def main():
     wall_max = float(t.item())
     wdl_total = [int(x) for x in wdl_total.cpu().tolist()]
 
+    # the same play one ply per launch: every ply's state round-trips HBM (the
+    # north-star kernel shape); reported beside the headline, not as `value`
+    single = None
+    if not args.no_single_ply and world == 1:
+        a1 = torch.empty(1, E, dtype=torch.int32, device=dev)
+        r1 = torch.empty(1, E, dtype=torch.int32, device=dev)
+        d1 = torch.empty(1, E, dtype=torch.uint8, device=dev)
+        for _ in range(50):
+            env.step_policy(args.policy, n_plies=1, actions=a1, rewards=r1, dones=d1)
+        torch.cuda.synchronize()
+        k1 = 500
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(k1):
+            env.step_policy(args.policy, n_plies=1, actions=a1, rewards=r1, dones=d1)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / k1
+        b1 = algorithmic_bytes_per_launch(E, W, 1, True)
+        single = {"value": E / (us * 1e-6), "unit": "env-steps/s", "avg_launch_us": us,
+                  "algorithmic_bytes_per_launch": b1, "achieved_GBps": b1 / (us * 1e-6) / 1e9,
+                  "steps": k1}
+
     if rank == 0:
         total_steps = E * world * steps
         value = total_steps / wall_max
@@ -195,6 +219,7 @@ def main():
                              "note": "the kernel's real limiter: integer VALU issue (one wave per SIMD at "
                                      "65,536 boards), see DESIGN.md"}},
             "wdl": {"black_wins": wdl_total[0], "draws": wdl_total[1], "white_wins": wdl_total[2]},
+            "single_ply_launches": single,
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, n)

@@ -6,8 +6,10 @@ compiled once per N (-DOTH_N=4..16) in parallel, csrc/capi.hip holds the C
 ABI, and the objects are linked into one shared library."""
 import concurrent.futures
 import os
+import shutil
 import subprocess
 import sys
+import tempfile
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
@@ -36,8 +38,7 @@ def _jobs():
 def build(force=False, verbose=True, extra_flags=(), out=OUT, jobs=None):
     if not force and not needs_build(out):
         return out
-    objdir = os.path.join(os.path.dirname(out), "_objs", os.path.basename(out).replace(".so", ""))
-    os.makedirs(objdir, exist_ok=True)
+    objdir = tempfile.mkdtemp(prefix="oth_objs_")
     base = [HIPCC, "--offload-arch=%s" % ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall",
             "-Wno-pass-failed", "-I", os.path.join(ROOT, "include")] + list(extra_flags)
     units = [(os.path.join(CSRC, "capi.hip"), os.path.join(objdir, "capi.o"), [])]
@@ -54,10 +55,13 @@ def build(force=False, verbose=True, extra_flags=(), out=OUT, jobs=None):
 
     if verbose:
         print("hipcc %s -> %s (%d units, %s)" % (" ".join(base[1:]), out, len(units), objdir), flush=True)
-    with concurrent.futures.ThreadPoolExecutor(jobs or _jobs()) as ex:
-        objs = list(ex.map(compile_one, units))
-    subprocess.check_call([HIPCC, "--offload-arch=%s" % ARCH, "-shared", "-o", out + ".tmp"] + objs)
-    os.replace(out + ".tmp", out)
+    try:
+        with concurrent.futures.ThreadPoolExecutor(jobs or _jobs()) as ex:
+            objs = list(ex.map(compile_one, units))
+        subprocess.check_call([HIPCC, "--offload-arch=%s" % ARCH, "-shared", "-o", out + ".tmp"] + objs)
+        os.replace(out + ".tmp", out)
+    finally:
+        shutil.rmtree(objdir, ignore_errors=True)
     return out
 
 
