@@ -192,7 +192,7 @@ def main():
             workload += "-norecord"
         pmc = load_pmc(workload)
         out = {
-            "metric": METRIC if args.policy == "random" else "env-steps/sec (greedy policy, on-device argmax flips)",
+            "metric": METRIC if args.policy == "random" else "env-steps/sec (%s policy on device)" % args.policy,
             "value": value,
             "unit": "env-steps/s",
             "n_gpus": world,
