@@ -101,10 +101,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # test hooks for rehearsing the multi-process path on a one-GPU box:
+    # OTH_BENCH_DEVICE pins every rank to one device, OTH_BENCH_BACKEND=gloo
+    gpu = int(os.environ.get("OTH_BENCH_DEVICE", local))
+    backend = os.environ.get("OTH_BENCH_BACKEND", "nccl")
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
 
     from gymothelloenv_amd import VecOthelloEnv
     from gymothelloenv_amd.distributed import gather_wdl, shard
@@ -148,7 +155,7 @@ def main():
     wall = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1)  # HIP events on the launch stream
     wdl = env.counts()
-    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    t = torch.tensor([wall], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wdl_total = gather_wdl(wdl).sum(0)  # RCCL all-gather over xGMI: the W/D/L tally

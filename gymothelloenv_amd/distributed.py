@@ -31,9 +31,10 @@ def gather_wdl(counts, group=None):
         out = torch.empty(world * 3, dtype=torch.int64, device=counts.device)
         dist.all_gather_into_tensor(out, counts, group=group)
         return out.view(world, 3)
-    parts = [torch.empty_like(counts) for _ in range(world)]
-    dist.all_gather(parts, counts, group=group)
-    return torch.stack(parts)
+    host = counts.cpu()  # gloo: host tensors
+    parts = [torch.empty_like(host) for _ in range(world)]
+    dist.all_gather(parts, host, group=group)
+    return torch.stack(parts).to(counts.device)
 
 
 def total_wdl(counts, group=None):
