@@ -9,6 +9,7 @@ terminal/score) as HIP kernels for gfx950 behind a C ABI
     SimpleOthelloEnv,        reference's constructor / attributes / 4-tuple step
     OthelloEnv
     RandomPolicy, GreedyPolicy, MaxiMinPolicy, make_state, undo_state
+    masked_sample, masked_log_prob   policy-head sampling over legal squares
 """
 from ._lib import LIB_PATH, OthelloLibError, load  # noqa: F401
 
@@ -26,6 +27,9 @@ def __getattr__(name):
     if name in ("RandomPolicy", "GreedyPolicy", "MaxiMinPolicy"):
         from . import policies
         return getattr(policies, name)
+    if name in ("masked_sample", "masked_log_prob"):
+        from . import masked
+        return getattr(masked, name)
     if name in ("make_state", "undo_state"):
         from . import util
         return getattr(util, name)

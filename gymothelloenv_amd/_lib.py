@@ -27,10 +27,11 @@ OTH_OBS_BOARD_LEGAL = 1
 OTH_OBS_MAKE_STATE = 2
 OTH_OBS_ABSOLUTE = 3
 OTH_I8, OTH_I32, OTH_I64, OTH_F32, OTH_F64 = range(5)
+OTH_MASKED_SAMPLE, OTH_MASKED_MODE, OTH_MASKED_EVAL = range(3)
 
 # every symbol include/othello_mi355x.h declares: (restype, argtypes)
 _P = ctypes.c_void_p
-_I32, _U32, _U64 = ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64
+_I32, _U32, _U64, _I64 = ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int64
 SIGNATURES = {
     "oth_create": (_I32, [_I32, _I32, _U32, _U64, _U32, _I32, _I32, ctypes.POINTER(_P)]),
     "oth_destroy": (_I32, [_P]),
@@ -49,6 +50,8 @@ SIGNATURES = {
     "oth_set_player_turn": (_I32, [_P, _I32, _P, _P]),
     "oth_count_disks": (_I32, [_P, _P, _P]),
     "oth_counts": (_I32, [_P, _P, _I32, _P]),
+    "oth_masked_sample": (_I32, [_I32, _I32, _P, _I64, _P, _P, _U64, _U32, _U64, _I32, _P, _P, _P, _P]),
+    "oth_sample_actions": (_I32, [_P, _P, _I64, _P, _U64, _I32, _P, _P, _P, _P]),
     "oth_ply_counter": (_U64, [_P]),
     "oth_set_ply_counter": (_I32, [_P, _U64]),
     "oth_shape": (_I32, [_P, _P, _P, _P]),

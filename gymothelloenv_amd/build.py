@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 SIZES = list(range(4, 17))
-DEPS = [os.path.join(CSRC, f) for f in ("capi.hip", "kernels_n.hip", "device.hpp", "launch.hpp", "bitboard.hpp")] + \
+DEPS = [os.path.join(CSRC, f) for f in ("capi.hip", "kernels_n.hip", "masked.hip", "device.hpp", "launch.hpp", "bitboard.hpp")] + \
     [os.path.join(ROOT, "include", "othello_mi355x.h")]
 OUT = os.path.join(HERE, "liboth_mi355x.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -32,7 +32,7 @@ def needs_build(out=OUT):
 def _jobs():
     n = os.cpu_count() or 4
     cap = int(os.environ.get("MAX_JOBS", "16"))
-    return max(1, min(n, cap, len(SIZES) + 1))
+    return max(1, min(n, cap, len(SIZES) + 2))
 
 
 def build(force=False, verbose=True, extra_flags=(), out=OUT, jobs=None):
@@ -41,7 +41,8 @@ def build(force=False, verbose=True, extra_flags=(), out=OUT, jobs=None):
     objdir = tempfile.mkdtemp(prefix="oth_objs_")
     base = [HIPCC, "--offload-arch=%s" % ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall",
             "-Wno-pass-failed", "-I", os.path.join(ROOT, "include")] + list(extra_flags)
-    units = [(os.path.join(CSRC, "capi.hip"), os.path.join(objdir, "capi.o"), [])]
+    units = [(os.path.join(CSRC, "capi.hip"), os.path.join(objdir, "capi.o"), []),
+             (os.path.join(CSRC, "masked.hip"), os.path.join(objdir, "masked.o"), [])]
     units += [(os.path.join(CSRC, "kernels_n.hip"), os.path.join(objdir, "kernels_n%d.o" % n), ["-DOTH_N=%d" % n])
               for n in SIZES]
 

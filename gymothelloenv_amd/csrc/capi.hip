@@ -147,7 +147,7 @@ int oth_create(int32_t n_envs, int32_t board_size, uint32_t flags, uint64_t seed
     hipError_t err = hipMalloc((void**)&env->boards, E * 2 * W * sizeof(uint64_t));
     if (err == hipSuccess) err = hipMalloc((void**)&env->meta, ((E * sizeof(uint16_t) + 15) / 16) * 16);
     if (err == hipSuccess) err = hipMalloc((void**)&env->legal, E * W * sizeof(uint64_t));
-    env->nslots = (int32_t)((2 * E + BLOCK - 1) / BLOCK);  // the widest grid (Pair: 2 lanes per board)
+    env->nslots = (int32_t)((2 * E + BLOCK - 1) / BLOCK);  // the widest grid (Duo: 2 lanes per board)
     const size_t slot_bytes = (size_t)env->nslots * 4 * sizeof(unsigned long long);
     if (err == hipSuccess) err = hipMalloc((void**)&env->wdl, slot_bytes);
     if (err == hipSuccess) err = hipMemset(env->wdl, 0, slot_bytes);
@@ -264,6 +264,26 @@ int oth_legal_moves(int32_t board_size, int32_t n, const uint64_t* mover, const 
     });
 }
 
+
+int oth_masked_sample(int32_t board_size, int32_t n, const float* logits, int64_t ld, const uint64_t* legal,
+                      const float* uniforms, uint64_t seed, uint32_t id_base, uint64_t counter, int32_t mode,
+                      int32_t* actions, float* log_probs, float* entropy, oth_stream_t stream) {
+    const int bs = board_size < 4 ? 4 : board_size;
+    if (bs > 16) return fail(OTH_EINVAL, "board_size must be <= 16");
+    if (mode < OTH_MASKED_SAMPLE || mode > OTH_MASKED_EVAL) return fail(OTH_EINVAL, "unknown mode");
+    if (n < 0 || (n > 0 && (!logits || !legal || !actions))) return fail(OTH_EINVAL, "bad arguments");
+    if (ld < (int64_t)bs * bs) return fail(OTH_EINVAL, "ld < board_size^2");
+    if (n == 0) return OTH_OK;
+    return launch_masked(bs, n, logits, (long long)ld, legal, uniforms, seed, id_base, counter, mode, actions,
+                         log_probs, entropy, (hipStream_t)stream);
+}
+
+int oth_sample_actions(oth_env* env, const float* logits, int64_t ld, const float* uniforms, uint64_t counter,
+                       int32_t mode, int32_t* actions, float* log_probs, float* entropy, oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    return oth_masked_sample(env->n, env->E, logits, ld, env->legal, uniforms, env->seed, env->id_base, counter, mode,
+                             actions, log_probs, entropy, stream);
+}
 
 int oth_observe(oth_env* env, int32_t layout, int32_t dtype, void* out, oth_stream_t stream) {
     OTH_CHECK_ENV(env);

@@ -1,5 +1,5 @@
 // device.hpp -- HIP/CDNA4 device code of the vectorised Othello rules engine:
-// per-lane board state, the rule engines (Solo / Rays / Pair), policies and
+// per-lane board state, the rule engines (Solo / Rays / Duo), policies and
 // every __global__ kernel template.  Included by kernels_n.hip (compiled once
 // per board size N, so the templates build in parallel) and by capi.hip.
 //
@@ -29,8 +29,8 @@
 
 using namespace oth;
 
-#ifndef OTH_PAIR
-#define OTH_PAIR 0  // 1: two lanes per board for N <= 8 in k_play (measured slower)
+#ifndef OTH_DUO
+#define OTH_DUO 0  // 1: Duo engine (two lanes per board, split axes + rays) for random play, N <= 8
 #endif
 #ifndef OTH_RAYS
 #define OTH_RAYS 1  // LDS ray-table flips for N <= 8 in k_play
@@ -120,10 +120,11 @@ __device__ __forceinline__ void store_lane(const Lane<N>& s, uint64_t* __restric
 // ---------------------------------------------------------------------------
 // Engines: who computes legal moves and flips for a lane.
 //   Solo<N>: one lane per board, all 8 directions (any N).
-//   Pair<N>: two lanes per board (N <= 8, one word): each lane of the pair
-//            scans 4 of the 8 directions and the halves are or-ed through a DPP
-//            quad_perm swap.  Twice the waves for the same boards, so two waves
-//            share each SIMD's issue slots instead of one wave issuing alone.
+//   Rays<N>: Solo with LDS ray-table flips (N <= 8).
+//   Duo<N>:  two lanes per board (N <= 8): each lane of the pair scans half
+//            the directions and the halves are or-ed through a DPP quad_perm
+//            swap.  Twice the waves for the same boards, so two waves share
+//            each SIMD's issue slots instead of one wave issuing alone.
 // ---------------------------------------------------------------------------
 template <int N>
 struct Solo {
@@ -210,72 +211,76 @@ __device__ __forceinline__ uint64_t pair_swap(uint64_t x) {
     return ((uint64_t)pair_swap32((uint32_t)(x >> 32)) << 32) | pair_swap32((uint32_t)x);
 }
 
+// Duo<N>: two lanes per board (N <= 8, one word); each lane runs the Solo/Rays
+// algorithms on half the geometry: lane 0 the E/W and S/N axes, lane 1 the two
+// diagonal axes (legal_axis with per-lane shift amounts), and the ray-table
+// flips of its four directions.  Every decision of step_lane is taken on the
+// or-ed (pair-uniform) masks, so both lanes of a pair always follow the same
+// branches and the DPP swap never reads an inactive lane.
 template <int N>
-struct Pair {
-    static_assert(Geo<N>::W == 1, "Pair engine is for one-word boards (N <= 8)");
+struct Duo {
+    static_assert(Geo<N>::W == 1, "Duo engine is for one-word boards (N <= 8)");
     static constexpr int LANES = 2;
+    static constexpr int RAY_WORDS = 8 * 64;
     static constexpr int STEPS = Pro<N, 0, 1>::STEPS;
-    static constexpr uint64_t NC0 = Geo<N>::NOT_COL0.w[0], NCN = Geo<N>::NOT_COLN1.w[0], BD = Geo<N>::BOARD.w[0];
-    // Direction k of this lane: k even shifts toward higher squares, k odd toward lower.
-    //   lane 0: +1 (E), -1 (W), +N (S), -N (N)
-    //   lane 1: +(N+1) (SE), -(N+1) (NW), +(N-1) (SW), -(N-1) (NE)
-    // The dst masks of k = 0, 1 are the same for both lanes; k = 2, 3 are per lane.
-    uint32_t sA, sB;    // shift of k = 0/1 and of k = 2/3
-    uint64_t m2, m3;    // dst masks of k = 2 and k = 3
+    static constexpr uint64_t BD = Geo<N>::BOARD.w[0], IN = Geo<N>::INNER.w[0];
+    const uint64_t* rays;  // this lane's first "up" table (E or SE)
+    uint32_t sA, sB;       // axis shifts: lane 0 {1, N}, lane 1 {N+1, N-1}
+    uint64_t mB;           // propagator mask of axis B: the vertical axis may pass edge columns
     int h;
-    static constexpr int RAY_WORDS = 0;
-    __device__ __forceinline__ Pair(int lane_half, const uint64_t*) : h(lane_half) {
-        sA = h ? N + 1 : 1;
-        sB = h ? N - 1 : N;
-        m2 = h ? NCN : BD;
-        m3 = h ? NC0 : BD;
+    __device__ __forceinline__ Duo(int lane_half, const uint64_t* lds) : h(lane_half) {
+        rays = lds + 128 * lane_half;
+        sA = lane_half ? N + 1 : 1;
+        sB = lane_half ? N - 1 : N;
+        mB = lane_half ? IN : BD;
     }
-    template <bool UP>
-    __device__ __forceinline__ static uint64_t sh(uint64_t x, uint32_t s) {
-        return UP ? (x << s) : (x >> s);
-    }
-    // opponent run next to generator g along (shift s, mask m), Kogge-Stone
-    template <bool UP>
-    __device__ __forceinline__ static uint64_t run(uint64_t g, uint64_t O, uint32_t s, uint64_t m) {
-        const uint64_t p1 = O & m;
-        uint64_t t = sh<UP>(g, s) & p1;
-        t |= p1 & sh<UP>(t, s);
-        if constexpr (STEPS > 1) {
-            const uint64_t p2 = p1 & sh<UP>(p1, s);
-            t |= p2 & sh<UP>(t, 2 * s);
-            if constexpr (STEPS > 2) {
-                const uint64_t p4 = p2 & sh<UP>(p2, 2 * s);
-                t |= p4 & sh<UP>(t, 4 * s);
-            }
-        }
-        return t;
+    __device__ __forceinline__ static void axis(uint64_t P, uint64_t p1, uint32_t s, uint64_t& L) {
+        uint64_t p2 = 0, p4 = 0;
+        if constexpr (STEPS > 1) p2 = p1 & (p1 << s);
+        if constexpr (STEPS > 2) p4 = p2 & (p2 << (2 * s));
+        uint64_t t = (P << s) & p1;
+        t |= p1 & (t << s);
+        if constexpr (STEPS > 1) t |= p2 & (t << (2 * s));
+        if constexpr (STEPS > 2) t |= p4 & (t << (4 * s));
+        L |= t << s;
+        t = (P >> s) & p1;
+        t |= p1 & (t >> s);
+        if constexpr (STEPS > 1) t |= (p2 >> s) & (t >> (2 * s));
+        if constexpr (STEPS > 2) t |= (p4 >> (3 * s)) & (t >> (4 * s));
+        L |= t >> s;
     }
     __device__ __forceinline__ BB<1> legal(const BB<1>& Pb, const BB<1>& Ob) const {
         const uint64_t P = Pb.w[0], O = Ob.w[0];
-        uint64_t L = sh<true>(run<true>(P, O, sA, NC0), sA) & NC0;
-        L |= sh<false>(run<false>(P, O, sA, NCN), sA) & NCN;
-        L |= sh<true>(run<true>(P, O, sB, m2), sB) & m2;
-        L |= sh<false>(run<false>(P, O, sB, m3), sB) & m3;
+        uint64_t L = 0;
+        axis(P, O & IN, sA, L);
+        axis(P, O & mB, sB, L);
         L |= pair_swap(L);
         BB<1> r;
         r.w[0] = L & ~(P | O) & BD;
         return r;
     }
     __device__ __forceinline__ BB<1> flip(const BB<1>& Pb, const BB<1>& Ob, int a) const {
-        const uint64_t P = Pb.w[0], O = Ob.w[0], m = 1ull << a;
-        uint64_t f = 0, t;
-        t = run<true>(m, O, sA, NC0);
-        f |= (sh<true>(t, sA) & P & NC0) ? t : 0ull;
-        t = run<false>(m, O, sA, NCN);
-        f |= (sh<false>(t, sA) & P & NCN) ? t : 0ull;
-        t = run<true>(m, O, sB, m2);
-        f |= (sh<true>(t, sB) & P & m2) ? t : 0ull;
-        t = run<false>(m, O, sB, m3);
-        f |= (sh<false>(t, sB) & P & m3) ? t : 0ull;
+        const uint64_t P = Pb.w[0], nO = ~Ob.w[0];
+        const uint64_t* r = rays + a;
+        uint64_t f = 0;
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {  // toward higher squares: E, S | SE, SW
+            const uint64_t ray = r[64 * d];
+            const uint64_t x = ray & nO;
+            const uint64_t fb = x & (0ull - x);
+            f |= (fb & P) ? (ray & (fb - 1ull)) : 0ull;
+        }
+#pragma unroll
+        for (int d = 4; d < 6; ++d) {  // toward lower squares: W, N | NW, NE
+            const uint64_t ray = r[64 * d];
+            const uint64_t x = ray & nO;
+            const uint64_t hb = x ? (0x8000000000000000ull >> __clzll(x)) : 0ull;
+            f |= (hb & P) ? (ray & (0ull - (hb << 1))) : 0ull;
+        }
         f |= pair_swap(f);
-        BB<1> r;
-        r.w[0] = f;
-        return r;
+        BB<1> out;
+        out.w[0] = f;
+        return out;
     }
     __device__ __forceinline__ bool leader() const { return h == 0; }
 };
@@ -412,18 +417,11 @@ __device__ __forceinline__ void greedy_scan(const Lane<N>& s, int parity, int st
     }
 }
 
-// With a Pair engine each lane scores every other candidate (by rank), then
-// the pair keeps the larger count, the lower square on a tie.
 template <int N, typename Eng>
 __device__ __forceinline__ int greedy_action(const Lane<N>& s, const Eng& eng) {
+    static_assert(Eng::LANES == 1, "greedy runs one lane per board");
     int best, cnt;
-    if constexpr (Eng::LANES == 1) {
-        greedy_scan<N>(s, 0, 1, best, cnt, eng);
-    } else {
-        greedy_scan<N>(s, eng.h, 2, best, cnt, eng);
-        const int ob = (int)pair_swap32((uint32_t)best), oc = (int)pair_swap32((uint32_t)cnt);
-        if (oc > cnt || (oc == cnt && ob >= 0 && (best < 0 || ob < best))) best = ob;
-    }
+    greedy_scan<N>(s, 0, 1, best, cnt, eng);
     return best;
 }
 
@@ -594,7 +592,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(uint64_t* __restrict__ boards, u
 
 // oth_step_policy: `plies` plies of on-device play with the board kept in
 // registers between plies; per-ply outputs stored [ply][E].  Eng::LANES lanes
-// per board (Solo: 1, Pair: 2); only the pair's leader lane stores.
+// per board (Solo/Rays: 1, Duo: 2); only the pair's leader lane stores.
 template <int N, int POLICY, typename Eng>
 __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
                                                 uint64_t* __restrict__ legal, int E, uint32_t flags, int plies,

@@ -55,8 +55,8 @@ int launch_play(oth_env* env, int policy, int n_plies, int32_t* actions, int32_t
                 uint64_t ply0, hipStream_t st) {
     return with_policy(policy, [&](auto PC) {
         constexpr int POL = decltype(PC)::value;
-        if constexpr (Geo<N>::W == 1 && OTH_PAIR && POL != OTH_POLICY_MAXIMIN2 && POL != OTH_POLICY_MAXIMIN3) {
-            hipLaunchKernelGGL((k_play<N, POL, Pair<N>>), dim3(grid_for(2ll * env->E)), dim3(BLOCK), 0, st,
+        if constexpr (Geo<N>::W == 1 && OTH_DUO && POL == OTH_POLICY_RANDOM) {
+            hipLaunchKernelGGL((k_play<N, POL, Duo<N>>), dim3(grid_for(2ll * env->E)), dim3(BLOCK), 0, st,
                                env->boards, env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards,
                                dones, env->wdl, rng_of(env), ply0);
         } else if constexpr (Geo<N>::W == 1 && OTH_RAYS && POL == OTH_POLICY_RANDOM) {

@@ -31,6 +31,11 @@ int fail(int code, const char* msg);
 int hip_fail(hipError_t err, const char* where);
 int after_launch(const char* what);
 
+// masked categorical (masked.hip), any board size
+int launch_masked(int n_board, int E, const float* logits, long long ld, const uint64_t* legal, const float* uniforms,
+                  uint64_t seed, uint32_t id_base, uint64_t counter, int mode, int32_t* actions, float* log_probs,
+                  float* entropy, hipStream_t st);
+
 // one set per board size N (kernels_n.hip instantiates them)
 template <int N> int launch_reset(oth_env* env, const uint8_t* mask, hipStream_t st);
 template <int N>

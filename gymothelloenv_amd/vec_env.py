@@ -69,6 +69,7 @@ class VecOthelloEnv(object):
                                          self.env_id_base, self.initial_rand_steps, self.device.index,
                                          ctypes.byref(h)), "oth_create")
         self._h = h
+        self._sample_calls = 0  # Philox counter of sample_actions
 
     # ------------------------------------------------------------------ utils
     def _stream(self):
@@ -254,16 +255,40 @@ class VecOthelloEnv(object):
         L.check(self._lib.oth_counts(self._h, _ptr(out), int(bool(reset)), self._stream()), "oth_counts")
         return out
 
+    def sample_actions(self, logits, deterministic=False, uniforms=None, log_probs=True, entropy=True):
+        """Policy.act (model.py:60-99) for every board at once: sample (or, when
+        deterministic, take the mode of) the softmax of `logits` (E, N*N)
+        float32 restricted to the board's possible_moves.  Draws are Philox
+        keyed (seed, env id, call counter) unless `uniforms` (E,) is given.
+        Returns (actions int32, log_probs, entropy) on the device; the actions
+        feed step() directly."""
+        from .masked import _rows
+        x = _rows(logits, self.board_size)
+        if x.shape[0] != self.num_envs:
+            raise ValueError("logits must have one row per board")
+        if uniforms is not None:
+            uniforms = uniforms.to(device=x.device, dtype=torch.float32).contiguous()
+        acts = self._i32(self.num_envs)
+        lp = torch.empty(self.num_envs, dtype=torch.float32, device=self.device) if log_probs else None
+        ent = torch.empty(self.num_envs, dtype=torch.float32, device=self.device) if entropy else None
+        mode = L.OTH_MASKED_MODE if deterministic else L.OTH_MASKED_SAMPLE
+        L.check(self._lib.oth_sample_actions(self._h, _ptr(x), x.stride(0), _ptr(uniforms), self._sample_calls,
+                                             mode, _ptr(acts), _ptr(lp), _ptr(ent), self._stream()),
+                "oth_sample_actions")
+        self._sample_calls += 1
+        return acts, lp, ent
+
     def state_dict(self):
         b, m, lg = self.get_state()
         return {"boards": b, "meta": m, "legal": lg, "ply_counter": self.ply_counter,
-                "board_size": self.board_size, "num_envs": self.num_envs}
+                "sample_calls": self._sample_calls, "board_size": self.board_size, "num_envs": self.num_envs}
 
     def load_state_dict(self, sd):
         if sd["board_size"] != self.board_size or sd["num_envs"] != self.num_envs:
             raise ValueError("state_dict shape does not match this env")
         self.set_state(sd["boards"], sd["meta"], sd["legal"])
         self.ply_counter = sd["ply_counter"]
+        self._sample_calls = int(sd.get("sample_calls", 0))
 
     # decoded views of the meta word
     def player_turn(self):

@@ -74,6 +74,13 @@ enum {
 /* observation element types */
 enum { OTH_I8 = 0, OTH_I32 = 1, OTH_I64 = 2, OTH_F32 = 3, OTH_F64 = 4 };
 
+/* masked-categorical modes (oth_masked_sample) */
+enum {
+    OTH_MASKED_SAMPLE = 0, /* FixedCategorical(...).sample() / np.random.choice: actions out */
+    OTH_MASKED_MODE = 1,   /* FixedCategorical(...).mode(): first largest legal logit; actions out */
+    OTH_MASKED_EVAL = 2    /* evaluate_actions: actions in, log-probs of those actions out */
+};
+
 /* OthelloBaseEnv.__init__ (othello.py:222-254) for n_envs boards of size
  * board_size (clamped to >= 4 like othello.py:230; > 16 is OTH_EINVAL).
  * seed / env_id_base key the Philox RNG of the on-device policies: env i uses
@@ -162,6 +169,31 @@ int oth_count_disks(oth_env *env, int32_t *out, oth_stream_t stream);
  * the last reset of the counters: out int64[3] = {black wins, draws, white
  * wins} (device pointer).  reset != 0 zeroes the counters after the copy. */
 int oth_counts(oth_env *env, int64_t *out, int32_t reset, oth_stream_t stream);
+
+/* Masked categorical over each board's legal squares (policy head of the
+ * learners; replaces the per-sample loops of
+ * pytorch_a2c_ppo_acktr_gail/a2c_ppo_acktr/model.py:60-99 Policy.act,
+ * model.py:156-178 Policy.evaluate_actions and ppo.py:228-298 PPO.get_action).
+ * n boards: logits float32 rows of N*N with row stride ld (elements), legal
+ * uint64[n][W] (e.g. oth_legal's output), device pointers.
+ *   OTH_MASKED_SAMPLE: action = the first legal square whose cumulative
+ *     softmax mass exceeds u * total, u = uniforms[e] in [0,1) if uniforms is
+ *     non-NULL, else a Philox draw keyed (seed, id_base + e, counter);
+ *   OTH_MASKED_MODE: action = the lowest legal square of the largest logit;
+ *   OTH_MASKED_EVAL: actions is an INPUT.
+ * log_probs[e] = log softmax over the legal squares at the action (0 when the
+ * board has no legal move or the action is not one of them, model.py:69-71,
+ * :165); entropy[e] = entropy of the masked distribution (0 with no legal
+ * move).  A board without legal moves samples action 0 (model.py:69-71).
+ * log_probs / entropy may be NULL.  Logits must be finite. */
+int oth_masked_sample(int32_t board_size, int32_t n, const float *logits, int64_t ld, const uint64_t *legal,
+                      const float *uniforms, uint64_t seed, uint32_t id_base, uint64_t counter, int32_t mode,
+                      int32_t *actions, float *log_probs, float *entropy, oth_stream_t stream);
+
+/* oth_masked_sample over the handle's own boards and possible_moves, keyed
+ * by the handle's seed and env ids. */
+int oth_sample_actions(oth_env *env, const float *logits, int64_t ld, const float *uniforms, uint64_t counter,
+                       int32_t mode, int32_t *actions, float *log_probs, float *entropy, oth_stream_t stream);
 
 /* Global ply counter of the handle (the Philox counter of the next ply). */
 uint64_t oth_ply_counter(const oth_env *env);

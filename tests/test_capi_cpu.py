@@ -55,6 +55,14 @@ def test_invalid_arguments_fail_without_gpu(lib):
     assert lib.oth_reset(None, None, None) == -1
     assert lib.oth_legal_moves(8, -1, None, None, None, None) == -1
     assert lib.oth_legal_moves(8, 0, None, None, None, None) == 0
+    ms = lib.oth_masked_sample
+    assert ms(17, 4, None, 289, None, None, 0, 0, 0, 0, None, None, None, None) == -1
+    assert ms(8, 4, None, 64, None, None, 0, 0, 0, 3, None, None, None, None) == -1
+    assert b"mode" in lib.oth_last_error()
+    assert ms(8, 4, None, 64, None, None, 0, 0, 0, 0, None, None, None, None) == -1
+    assert ms(8, 0, None, 63, None, None, 0, 0, 0, 0, None, None, None, None) == -1  # ld < N*N
+    assert ms(8, 0, None, 64, None, None, 0, 0, 0, 0, None, None, None, None) == 0
+    assert lib.oth_sample_actions(None, None, 64, None, 0, 0, None, None, None, None) == -1
 
 
 def test_mask_conversions():

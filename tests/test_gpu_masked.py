@@ -1,0 +1,212 @@
+"""Masked categorical over legal squares (csrc/masked.hip)
+against a float64 numpy restatement of the learners' per-sample loops
+(model.py:60-99 act, :156-178 evaluate_actions; ppo.py:228-298 get_action)
+and torch's own Categorical (the reference's FixedCategorical base class).
+
+Tolerances (fp32 kernel vs fp64 restatement): log-probs and entropies
+atol 2e-5 + rtol 1e-5; a sampled square may differ from the fp64 choice only
+when u * total lies within 1e-5 * total of a cumulative-mass boundary."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [4, 5, 6, 7, 8, 10, 16]
+ATOL, RTOL, CDF_TOL = 2e-5, 1e-5, 1e-5
+
+
+@pytest.fixture(scope="module")
+def torch_gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def pack(legal_bool):
+    """(n, N*N) bool -> (n, W) int64 bit masks (bit a of word a // 64 = square a)."""
+    n, nn = legal_bool.shape
+    w = (nn + 63) // 64
+    out = np.zeros((n, w), dtype=np.uint64)
+    for a in range(nn):
+        out[:, a // 64] |= legal_bool[:, a].astype(np.uint64) << np.uint64(a % 64)
+    return out.view(np.int64)
+
+
+def make_case(rng, n, nn):
+    logits = (rng.standard_normal((n, nn)) * 3).astype(np.float32)
+    legal = rng.random((n, nn)) < rng.uniform(0.05, 0.5, size=(n, 1))
+    legal[: n // 16] = False                    # no legal move
+    one = slice(n // 16, n // 8)                # exactly one legal move
+    legal[one] = False
+    legal[one, rng.integers(0, nn, size=n // 8 - n // 16)] = True
+    ties = slice(n // 8, n // 8 + n // 32)      # equal logits: mode takes the lowest square
+    logits[ties] = 1.25
+    return logits, legal
+
+
+def ref_masked(logits, legal, u):
+    """fp64 restatement: masked softmax, first-max mode, np.random.choice's
+    searchsorted(cdf, u * total, 'right'), log-prob and entropy."""
+    x = logits.astype(np.float64)
+    anyl = legal.any(1)
+    m = np.where(legal, x, -np.inf).max(1)
+    m = np.where(anyl, m, 0.0)
+    p = np.where(legal, np.exp(x - m[:, None]), 0.0)
+    S = p.sum(1)
+    lse = m + np.log(np.where(anyl, S, 1.0))
+    mode = np.argmax(np.where(legal, x, -np.inf), axis=1)
+    cdf = np.cumsum(p, 1)
+    target = u * S
+    hit = (cdf > target[:, None]) & legal
+    samp = np.where(hit.any(1), np.argmax(hit, 1), legal.shape[1] - 1 - np.argmax(legal[:, ::-1], 1))
+    mode = np.where(anyl, mode, 0)
+    samp = np.where(anyl, samp, 0)
+    ent = np.where(anyl, -(np.where(legal, p / np.where(anyl, S, 1.0)[:, None], 0.0) *
+                           np.where(legal, x - lse[:, None], 0.0)).sum(1), 0.0)
+    return dict(mode=mode, samp=samp, lse=lse, ent=ent, cdf=cdf, p=p, S=S, target=target, x=x, anyl=anyl)
+
+
+def lp_of(ref, legal, a):
+    rows = np.arange(len(a))
+    ok = ref["anyl"] & (a >= 0) & (a < legal.shape[1])
+    ok[ok] &= legal[rows[ok], a[ok]]
+    return np.where(ok, ref["x"][rows, np.clip(a, 0, legal.shape[1] - 1)] - ref["lse"], 0.0)
+
+
+@pytest.mark.parametrize("n_board", SIZES)
+def test_masked_matches_fp64_restatement(torch_gpu, n_board):
+    torch = torch_gpu
+    from gymothelloenv_amd import masked_log_prob, masked_sample
+    rng = np.random.default_rng(n_board)
+    n, nn = 4096, n_board * n_board
+    logits, legal = make_case(rng, n, nn)
+    u = rng.random(n).astype(np.float32)
+    ref = ref_masked(logits, legal, u.astype(np.float64))
+    dl = torch.from_numpy(logits).cuda()
+    dg = torch.from_numpy(pack(legal)).cuda()
+    # mode
+    a, lp, ent = masked_sample(dl, dg, n_board, mode="mode")
+    a = a.cpu().numpy()
+    np.testing.assert_array_equal(a, ref["mode"])
+    np.testing.assert_allclose(lp.cpu().numpy(), lp_of(ref, legal, a), atol=ATOL, rtol=RTOL)
+    np.testing.assert_allclose(ent.cpu().numpy(), ref["ent"], atol=ATOL, rtol=RTOL)
+    # sample with the caller's uniforms
+    a, lp, ent = masked_sample(dl, dg, n_board, uniforms=torch.from_numpy(u).cuda())
+    a = a.cpu().numpy()
+    rows = np.arange(n)
+    bad = np.flatnonzero(a != ref["samp"])
+    assert len(bad) <= n // 200, len(bad)
+    for i in bad:  # only boundary cases, and always a legal square whose mass interval holds u * total
+        g = a[i]
+        assert legal[i, g]
+        hi, lo = ref["cdf"][i, g], ref["cdf"][i, g] - ref["p"][i, g]
+        tol = CDF_TOL * ref["S"][i]
+        assert lo - tol <= ref["target"][i] <= hi + tol, (i, g, ref["samp"][i])
+    np.testing.assert_allclose(lp.cpu().numpy(), lp_of(ref, legal, a), atol=ATOL, rtol=RTOL)
+    assert (a[~ref["anyl"]] == 0).all() and (lp.cpu().numpy()[~ref["anyl"]] == 0).all()
+    assert legal[rows[ref["anyl"]], a[ref["anyl"]]].all()
+    # evaluate_actions: arbitrary actions incl. illegal / out of range -> 0
+    acts = rng.integers(-2, nn + 2, size=n).astype(np.int32)
+    acts[: n // 2] = ref["samp"][: n // 2]
+    lp2, ent2 = masked_log_prob(dl, dg, torch.from_numpy(acts).cuda(), n_board)
+    np.testing.assert_allclose(lp2.cpu().numpy(), lp_of(ref, legal, acts), atol=ATOL, rtol=RTOL)
+    np.testing.assert_allclose(ent2.cpu().numpy(), ref["ent"], atol=ATOL, rtol=RTOL)
+
+
+def test_log_prob_matches_torch_categorical(torch_gpu):
+    """FixedCategorical (the reference's distribution class) is torch's
+    Categorical: compare its fp32 log_prob / entropy row by row."""
+    torch = torch_gpu
+    from gymothelloenv_amd import masked_sample
+    rng = np.random.default_rng(7)
+    logits, legal = make_case(rng, 512, 64)
+    a, lp, ent = masked_sample(torch.from_numpy(logits).cuda(), torch.from_numpy(pack(legal)).cuda(), 8)
+    a, lp, ent = a.cpu().numpy(), lp.cpu().numpy(), ent.cpu().numpy()
+    for i in range(512):
+        idx = np.flatnonzero(legal[i])
+        if len(idx) == 0:
+            assert a[i] == 0 and lp[i] == 0 and ent[i] == 0
+            continue
+        d = torch.distributions.Categorical(logits=torch.from_numpy(logits[i, idx]))
+        k = int(np.flatnonzero(idx == a[i])[0])
+        assert abs(float(d.log_prob(torch.tensor(k))) - lp[i]) <= ATOL + RTOL * abs(lp[i])
+        assert abs(float(d.entropy()) - ent[i]) <= ATOL + RTOL * abs(ent[i])
+
+
+def test_philox_sampling_distribution(torch_gpu):
+    """Philox-keyed sampling of one distribution over 262,144 boards follows
+    the masked softmax; repeat calls with the same key agree, a new counter
+    draws afresh."""
+    torch = torch_gpu
+    from gymothelloenv_amd import masked_sample
+    n = 262144
+    row = np.linspace(-2.0, 2.0, 64).astype(np.float32)
+    legal = np.zeros(64, bool)
+    legal[[0, 3, 9, 20, 27, 36, 44, 50, 61, 63]] = True
+    dl = torch.from_numpy(np.tile(row, (n, 1))).cuda()
+    dg = torch.from_numpy(pack(np.tile(legal, (n, 1)))).cuda()
+    a1, _, _ = masked_sample(dl, dg, 8, seed=5, counter=1)
+    a2, _, _ = masked_sample(dl, dg, 8, seed=5, counter=1)
+    a3, _, _ = masked_sample(dl, dg, 8, seed=5, counter=2)
+    assert torch.equal(a1, a2) and not torch.equal(a1, a3)
+    a1 = a1.cpu().numpy()
+    assert legal[a1].all()
+    p = np.exp(row[legal] - row[legal].max())
+    p /= p.sum()
+    freq = np.bincount(a1, minlength=64)[legal] / n
+    assert np.abs(freq - p).max() < 5 * np.sqrt(p.max() / n)
+
+
+def test_strided_and_unaligned_rows(torch_gpu):
+    """Row stride > N*N (ld) and rows not 16-byte aligned (scalar-load path)."""
+    torch = torch_gpu
+    from gymothelloenv_amd import masked_sample
+    rng = np.random.default_rng(3)
+    logits, legal = make_case(rng, 1024, 64)
+    u = torch.from_numpy(rng.random(1024).astype(np.float32)).cuda()
+    dg = torch.from_numpy(pack(legal)).cuda()
+    base = masked_sample(torch.from_numpy(logits).cuda(), dg, 8, uniforms=u)
+    wide = torch.zeros(1024, 81, dtype=torch.float32, device="cuda")  # ld 81, rows start at column 1
+    wide[:, 1:65] = torch.from_numpy(logits).cuda()
+    pad = torch.zeros(1024, 80, dtype=torch.float32, device="cuda")   # ld 80, 16-byte aligned rows
+    pad[:, :64] = torch.from_numpy(logits).cuda()
+    for view in (wide[:, 1:65], pad[:, :64]):
+        got = masked_sample(view, dg, 8, uniforms=u)
+        assert torch.equal(got[0], base[0])
+        torch.testing.assert_close(got[1], base[1], atol=1e-6, rtol=0)
+
+
+def test_env_rollout_with_sampled_actions(torch_gpu):
+    """VecOthelloEnv.sample_actions feeds step() directly: every sampled move is
+    legal, so no game ends by sudden death, and the boards still replay
+    bit-exactly through the CPU oracle."""
+    torch = torch_gpu
+    from gymothelloenv_amd import VecOthelloEnv
+    from oracle import oracle
+    E = 2048
+    env = VecOthelloEnv(E, board_size=8, seed=11, device="cuda:0")
+    twin = VecOthelloEnv(E, board_size=8, seed=11, device="cuda:0")
+    env.reset()
+    twin.reset()
+    s = oracle.reset(8, E)
+    g = torch.Generator(device="cuda").manual_seed(0)
+    for ply in range(70):
+        logits = torch.randn(E, 64, device="cuda", generator=g) * 2
+        legal = env.legal_mask().cpu().numpy().view(np.uint64)[:, 0]
+        a, lp, ent = env.sample_actions(logits)
+        assert torch.equal(a, twin.sample_actions(logits)[0])  # same key -> same draws
+        an = a.cpu().numpy()
+        live = (s.meta & 2) == 0
+        has = legal != 0
+        assert all((int(legal[i]) >> int(an[i])) & 1 for i in np.flatnonzero(live & has))
+        assert (lp.cpu().numpy()[live & has] <= 0).all()
+        act = np.where(live, an, 0).astype(np.int32)
+        _, r, d, _ = env.step(torch.from_numpy(act).cuda(), observe=False)
+        twin.step(torch.from_numpy(act).cuda(), observe=False)
+        rr, dd, _ = oracle.step(s, oracle.F_SUDDEN_DEATH, act)
+        np.testing.assert_array_equal(r.cpu().numpy(), rr)
+        b, m, lg = env.get_state()
+        np.testing.assert_array_equal(b.cpu().numpy().view(np.uint64), s.boards)
+        np.testing.assert_array_equal(lg.cpu().numpy().view(np.uint64), s.legal)
+    assert (s.meta & 2).all()  # every game finished within 70 plies, none by an illegal move
