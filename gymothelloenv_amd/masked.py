@@ -55,13 +55,13 @@ def _check_legal(legal, n, board_size):
 
 
 def masked_sample(logits, legal, board_size, mode="sample", uniforms=None, seed=0, id_base=0, counter=0,
-                  log_probs=True, entropy=True):
+                  log_probs=True, entropy=True, lib=None):
     """Sample (or take the mode of) the masked categorical of every row.
 
     logits (n, N*N) float32, legal (n, W) int64 bit masks, both on one GPU;
     uniforms: optional (n,) float32 in [0, 1).  Returns (actions int32,
     log_probs float32 or None, entropy float32 or None)."""
-    lib = L.load()
+    lib = lib if lib is not None else L.load()
     bs = max(4, int(board_size))
     x = _rows(logits, bs)
     n = x.shape[0]
