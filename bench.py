@@ -16,8 +16,10 @@ Rank 0 prints one JSON line.  `roofline` prices the dominant kernel
 (k_play<8, random>) by its algorithmic HBM bytes per launch over its average
 launch time (HIP events on the launch stream); `traffic` comes from the
 rocprofv3 PMC summary committed under profiles/ (null if absent).
-`cpu_baseline` times the oracle's scalar restatement of othello.py on a host
-core over a bounded sample.
+`cpu_baseline` times the oracle's scalar restatement of othello.py on the
+host cores (one batch of boards per thread) over a bounded sample.
+`masked_sample` is a side measurement of the learners' masked-categorical
+kernel against the HBM peak.
 """
 import argparse
 import json
@@ -41,27 +43,52 @@ def algorithmic_bytes_per_launch(E, W, plies, record=True):
     return E * (state + plies * per_ply)
 
 
-def cpu_baseline(seconds, board_size=8):
+def cpu_threads():
+    """Host cores this process may use: the affinity set, capped by the job's
+    thread budget (OMP_NUM_THREADS is the box's CPU share)."""
+    n = len(os.sched_getaffinity(0))
+    cap = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(cap))) if cap and cap.isdigit() else n
+
+
+def cpu_baseline(seconds, board_size=8, threads=None):
     """Scalar restatement of the reference rules engine (oracle/, the per-cell
     8-direction ray walk of othello.py:273-343) with the same random policy and
-    auto-reset, single-threaded; bounded sample of ~`seconds` of CPU work."""
+    auto-reset, one independent batch of boards per host thread (the ctypes
+    call releases the GIL); a bounded sample of about `seconds` CPU-seconds
+    (at least 2 s of wall time)."""
+    import concurrent.futures
+    import threading
+
     from oracle import oracle
+    T = threads or cpu_threads()
     E, chunk = 1024, 16
-    s = oracle.reset(board_size, E)
+    wall = max(2.0, seconds / T)
     flags = oracle.F_SUDDEN_DEATH | oracle.F_AUTO_RESET
-    plies = 0
-    t0 = time.perf_counter()
-    while True:
-        oracle.rollout(s, flags, 0, chunk, seed=0, ply0=plies, record=False)
-        plies += chunk
-        dt = time.perf_counter() - t0
-        if dt >= seconds:
-            break
-    steps = E * plies
-    return {"value": steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": "%d boards x %d plies (%d env-steps) of random play, %dx%d, auto-reset, "
-                      "oracle/othello_oracle.c scalar ray-scan restatement of othello.py, 1 thread, %.1f s"
-                      % (E, plies, steps, board_size, board_size, dt)}
+    start = threading.Barrier(T + 1)
+
+    def worker(k):
+        s = oracle.reset(board_size, E)
+        plies = 0
+        start.wait()
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < wall:
+            oracle.rollout(s, flags, 0, chunk, seed=0, id_base=k * E, ply0=plies, record=False)
+            plies += chunk
+        return plies, time.perf_counter() - t0
+
+    with concurrent.futures.ThreadPoolExecutor(T) as ex:
+        futs = [ex.submit(worker, k) for k in range(T)]
+        start.wait()
+        res = [f.result() for f in futs]
+    steps = sum(E * p for p, _ in res)
+    dt = max(t for _, t in res)
+    return {"value": steps / dt, "unit": "env-steps/s", "cores": T, "kind": "port",
+            "per_core": steps / dt / T,
+            "sample": "%d threads x %d boards of random play, %dx%d, auto-reset, %d env-steps in %.1f s: "
+                      "oracle/othello_oracle.c scalar ray-scan restatement of othello.py (same per-cell "
+                      "8-direction walk as the reference), one batch per thread"
+                      % (T, E, board_size, board_size, steps, dt)}
 
 
 # VALU issue peak: 256 CUs x 4 SIMD32 x one wave64 instruction per 2 cycles at 2.4 GHz
@@ -93,6 +120,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single-ply", action="store_true", help="skip the one-ply-per-launch side measurement")
+    ap.add_argument("--no-masked", action="store_true", help="skip the masked-categorical side measurement")
     args = ap.parse_args()
 
     import torch
@@ -187,6 +215,39 @@ def main():
                   "algorithmic_bytes_per_launch": b1, "achieved_GBps": b1 / (us * 1e-6) / 1e9,
                   "steps": k1}
 
+    # side measurement: the learners' masked categorical (csrc/masked.hip) over
+    # 4,194,304 boards' fp32 logits (1.1 GB: beyond the 256 MiB Infinity Cache)
+    masked = None
+    if not args.no_masked and world == 1:
+        from gymothelloenv_amd import masked_sample
+        Em, nn = 4194304, n * n
+        g = torch.Generator(device=dev).manual_seed(0)
+        logits = torch.randn(Em, nn, device=dev, generator=g)
+        legal = env.legal_mask().repeat((Em + E - 1) // E, 1)[:Em].contiguous()
+        outs = [torch.empty(Em, dtype=torch.int32, device=dev)] + \
+            [torch.empty(Em, dtype=torch.float32, device=dev) for _ in range(2)]
+        lib = env._lib
+        import ctypes
+        args_m = lambda c: (n, Em, ctypes.c_void_p(logits.data_ptr()), nn, ctypes.c_void_p(legal.data_ptr()),
+                            None, 0, 0, c, 0, *[ctypes.c_void_p(o.data_ptr()) for o in outs],
+                            ctypes.c_void_p(stream.cuda_stream))
+        for c in range(3):
+            lib.oth_masked_sample(*args_m(c))
+        torch.cuda.synchronize()
+        km = 20
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for c in range(km):
+            lib.oth_masked_sample(*args_m(c))
+        e1.record(stream)
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / km
+        bm = Em * (4 * nn + 8 * W + 12)
+        masked = {"kernel": "k_masked", "boards": Em, "avg_launch_us": us, "algorithmic_bytes_per_launch": bm,
+                  "achieved_GBps": bm / (us * 1e-6) / 1e9, "frac_hbm_peak": bm / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS,
+                  "boards_per_s": Em / (us * 1e-6)}
+        del logits, legal, outs
+
     if rank == 0:
         total_steps = E * world * steps
         value = total_steps / wall_max
@@ -227,6 +288,7 @@ def main():
                                      "65,536 boards), see DESIGN.md"}},
             "wdl": {"black_wins": wdl_total[0], "draws": wdl_total[1], "white_wins": wdl_total[2]},
             "single_ply_launches": single,
+            "masked_sample": masked,
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, n)

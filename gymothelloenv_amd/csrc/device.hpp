@@ -32,6 +32,12 @@ using namespace oth;
 #ifndef OTH_DUO
 #define OTH_DUO 0  // 1: Duo engine (two lanes per board, split axes + rays) for random play, N <= 8
 #endif
+#ifndef OTH_FILLS
+#define OTH_FILLS 1  // Fills engine (ray tables + the legal scan's fills) for random play, N <= 8
+#endif
+#ifndef OTH_FILLS_GREEDY
+#define OTH_FILLS_GREEDY 1  // the Fills engine for greedy play too (0: Kogge-Stone flips)
+#endif
 #ifndef OTH_RAYS
 #define OTH_RAYS 1  // LDS ray-table flips for N <= 8 in k_play
 #endif
@@ -137,6 +143,7 @@ struct Solo {
     __device__ __forceinline__ BB<Geo<N>::W> flip(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O, int a) const {
         return flips<N>(P, O, square<Geo<N>::W>(a));
     }
+    __device__ __forceinline__ void prime(const Lane<N>&) const {}
     __device__ __forceinline__ bool leader() const { return true; }
 };
 
@@ -199,6 +206,93 @@ struct Rays {
         BB<1> out;
         out.w[0] = f;
         return out;
+    }
+    __device__ __forceinline__ void prime(const Lane<N>&) const {}
+    __device__ __forceinline__ bool leader() const { return true; }
+};
+
+// Fills<N>: Rays whose flips reuse the legal scan.  legal_moves' axis scans
+// compute, for the side to move, the fills t(dir) = opponent discs reachable
+// from an own disc through contiguous opponent discs stepping in direction dir
+// (the scan shifts them once more onto the empty squares).  Kept in registers
+// until the next ply, they answer update_board's capping test: along ray d
+// from the played square a, the run to flip is the contiguous part of ray_d(a)
+// inside t(-d) -- every square of t(-d) on that run is already capped by an
+// own disc further along d.  So per direction: nearest square of the ray NOT
+// in t(-d), and the ray squares before it; no test against the own discs.
+// The fills are valid for the board they were computed on: every path that
+// changes the side to move computes them (legal() in step_lane), and k_play
+// primes them after loading or resetting a board.
+template <int N>
+struct Fills {
+    static_assert(Geo<N>::W == 1, "fills engine is for one-word boards (N <= 8)");
+    static constexpr int LANES = 1;
+    static constexpr int RAY_WORDS = 8 * 64;
+    static constexpr int STEPS = Pro<N, 0, 1>::STEPS;
+    static constexpr uint64_t BD = Geo<N>::BOARD.w[0], IN = Geo<N>::INNER.w[0];
+    const uint64_t* rays;
+    // t[d] = the fill to use for ray direction d (rays: E, S, SE, SW, W, N, NW, NE):
+    // up directions (+S) use the -S fill, down directions the +S fill
+    mutable uint64_t t[8];
+    __device__ __forceinline__ Fills(int, const uint64_t* lds) : rays(lds) {}
+
+    template <int S>
+    __device__ __forceinline__ static void axis(uint64_t P, uint64_t p1, uint64_t& L, uint64_t& tplus,
+                                                uint64_t& tminus) {
+        uint64_t p2 = 0, p4 = 0;
+        if constexpr (STEPS > 1) p2 = p1 & (p1 << S);
+        if constexpr (STEPS > 2) p4 = p2 & (p2 << (2 * S));
+        uint64_t x = (P << S) & p1;
+        x |= p1 & (x << S);
+        if constexpr (STEPS > 1) x |= p2 & (x << (2 * S));
+        if constexpr (STEPS > 2) x |= p4 & (x << (4 * S));
+        tplus = x;
+        L |= x << S;
+        x = (P >> S) & p1;
+        x |= p1 & (x >> S);
+        if constexpr (STEPS > 1) x |= (p2 >> S) & (x >> (2 * S));
+        if constexpr (STEPS > 2) x |= (p4 >> (3 * S)) & (x >> (4 * S));
+        tminus = x;
+        L |= x >> S;
+    }
+    // get_possible_actions for mover P (legal_moves' axis-paired scan), keeping the fills
+    __device__ __forceinline__ BB<1> legal(const BB<1>& Pb, const BB<1>& Ob) const {
+        static_assert(Pro<N, 0, 1>::STEPS <= 3, "N <= 8");
+        const uint64_t P = Pb.w[0], O = Ob.w[0], pin = O & IN;
+        uint64_t L = 0;
+        axis<1>(P, pin, L, t[4], t[0]);          // W uses +1 fill, E uses -1 fill
+        axis<N>(P, O, L, t[5], t[1]);            // N / S
+        axis<N + 1>(P, pin, L, t[6], t[2]);      // NW / SE
+        axis<N - 1>(P, pin, L, t[7], t[3]);      // NE / SW
+        BB<1> r;
+        r.w[0] = L & ~(P | O) & BD;
+        return r;
+    }
+    __device__ __forceinline__ BB<1> flip(const BB<1>&, const BB<1>&, int a) const {
+        const uint64_t* r = rays + a;
+        uint64_t f = 0;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {  // toward higher squares: cap = lowest ray square outside the fill
+            const uint64_t ray = r[64 * d];
+            const uint64_t y = ray & ~t[d];
+            f |= ray & ((y & (0ull - y)) - 1ull);
+        }
+#pragma unroll
+        for (int d = 4; d < 8; ++d) {  // toward lower squares: cap = highest ray square outside the fill
+            // y == 0 only when the ray is empty (the edge square of a ray is never in a fill)
+            const uint64_t ray = r[64 * d];
+            const uint64_t y = (ray & ~t[d]) | 1ull;
+            const uint64_t hb = 0x8000000000000000ull >> __clzll(y);
+            f |= ray & (0ull - (hb << 1));
+        }
+        BB<1> out;
+        out.w[0] = f;
+        return out;
+    }
+    // recompute the fills for the side to move (after a load or a reset)
+    __device__ __forceinline__ void prime(const Lane<N>& s) const {
+        const bool tw = (s.meta & M_TURN_WHITE) != 0;
+        (void)legal(tw ? s.white : s.black, tw ? s.black : s.white);
     }
     __device__ __forceinline__ bool leader() const { return true; }
 };
@@ -282,6 +376,7 @@ struct Duo {
         out.w[0] = f;
         return out;
     }
+    __device__ __forceinline__ void prime(const Lane<N>&) const {}
     __device__ __forceinline__ bool leader() const { return h == 0; }
 };
 
@@ -610,6 +705,7 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
         const uint32_t id = rng.id_base + (uint32_t)e;
         Lane<N> s;
         load_lane<N>(s, boards, meta, legal, e);
+        eng.prime(s);
         U4 draws{0, 0, 0, 0};
         for (int p = 0; p < plies; ++p) {
             const uint64_t g = ply0 + (uint64_t)p;
@@ -643,8 +739,10 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
                     cb += win == BLACK_DISK;
                     cd += win == NO_DISK;
                     cw += win == WHITE_DISK;
-                    if (flags & OTH_AUTO_RESET)
+                    if (flags & OTH_AUTO_RESET) {
                         reset_lane<N>(s, rng.seed, id, g, RNG_OPENING_AUTO, rng.init_rand);
+                        eng.prime(s);
+                    }
                 }
             }
 #ifndef OTH_ABLATE_NOSTORE

@@ -59,10 +59,15 @@ int launch_play(oth_env* env, int policy, int n_plies, int32_t* actions, int32_t
             hipLaunchKernelGGL((k_play<N, POL, Duo<N>>), dim3(grid_for(2ll * env->E)), dim3(BLOCK), 0, st,
                                env->boards, env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards,
                                dones, env->wdl, rng_of(env), ply0);
+        } else if constexpr (Geo<N>::W == 1 && OTH_FILLS &&
+                             (POL == OTH_POLICY_RANDOM || (OTH_FILLS_GREEDY && POL == OTH_POLICY_GREEDY))) {
+            hipLaunchKernelGGL((k_play<N, POL, Fills<N>>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards,
+                               env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards, dones, env->wdl,
+                               rng_of(env), ply0);
         } else if constexpr (Geo<N>::W == 1 && OTH_RAYS && POL == OTH_POLICY_RANDOM) {
-            // random play: ray-table flips; the scripted policies keep Kogge-Stone
-            // flips in their candidate loops (the ray tables' exposed LDS latency
-            // measured -10 % for greedy)
+            // random play with OTH_FILLS=0: ray-table flips with the capping test
+            // (greedy keeps Kogge-Stone flips there: the ray tables' exposed LDS
+            // latency measured -10 % for greedy without the fills)
             hipLaunchKernelGGL((k_play<N, POL, Rays<N>>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards,
                                env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards, dones, env->wdl,
                                rng_of(env), ply0);
