@@ -134,6 +134,33 @@ def test_random_rollout_replays_on_oracle(torch_cuda, n, E, plies):
     assert owdl.sum() >= E  # at least one finished game per board
 
 
+@pytest.mark.parametrize("n,policy,sd,dr,auto,init_rand",
+                         [(4, "random", True, True, True, 0), (5, "random", False, True, True, 4),
+                          (7, "random", True, False, False, 0), (8, "random", False, False, True, 6),
+                          (4, "greedy", True, True, True, 2), (7, "greedy", False, False, True, 6),
+                          (5, "greedy", True, False, False, 4)])
+def test_fills_engine_flag_combinations(torch_cuda, n, policy, sd, dr, auto, init_rand):
+    """The fills engine (flips from the legal scan carried across plies) under
+    every flag combination, with and without auto-reset and random openings:
+    identical to the oracle's replay ply by ply."""
+    torch = torch_cuda
+    E, plies = 4096, 90
+    env = make_env(torch, E, n, sd=sd, dr=dr, auto=auto, seed=5, init_rand=init_rand)
+    env.reset()
+    acts, rews, dones = env.step_policy(policy, n_plies=plies)
+    b, m, lg = get_state_np(env)
+    s = oracle.reset_openings(n, E, 5, 0, 0, init_rand) if init_rand else oracle.reset(n, E)
+    pid = 0 if policy == "random" else 1
+    oa, orw, od, owdl = oracle.rollout(s, flags_of(sd, dr, auto), pid, plies, seed=5, initial_rand_steps=init_rand)
+    np.testing.assert_array_equal(acts.cpu().numpy(), oa)
+    np.testing.assert_array_equal(rews.cpu().numpy(), orw)
+    np.testing.assert_array_equal(dones.cpu().numpy(), od)
+    np.testing.assert_array_equal(b, s.boards)
+    np.testing.assert_array_equal(m, s.meta)
+    np.testing.assert_array_equal(lg, s.legal)
+    np.testing.assert_array_equal(env.counts().cpu().numpy(), owdl)
+
+
 def test_rollout_split_over_launches_is_identical(torch_cuda):
     """K plies in one launch == K single-ply launches (state round-trips HBM)."""
     torch = torch_cuda
