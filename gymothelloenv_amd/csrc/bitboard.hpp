@@ -241,6 +241,10 @@ struct Geo {
     }
 };
 
+#ifndef OTH_PROP_REUSE
+#define OTH_PROP_REUSE 1  // last doubling step reuses the previous propagator where it covers N - 2
+#endif
+
 #ifndef OTH_ANDOR
 #define OTH_ANDOR 0
 #endif
@@ -275,20 +279,29 @@ struct Pro {
     static constexpr int W = Geo<N>::W;
     static constexpr int S = DR * N + DC;
     static constexpr int STEPS = Geo<N>::MAXRUN > 8 ? 4 : (Geo<N>::MAXRUN > 4 ? 3 : (Geo<N>::MAXRUN > 2 ? 2 : 1));
+    // the last step reuses the previous propagator when that covers N - 2 (see legal_axis)
+    static constexpr bool R3 = OTH_PROP_REUSE && STEPS == 3 && Geo<N>::MAXRUN <= 6;
+    static constexpr bool R4 = OTH_PROP_REUSE && STEPS == 4 && Geo<N>::MAXRUN <= 12;
     BB<W> p1, p2, p4, p8;
     OTH_HD explicit Pro(const BB<W>& O) {
         p1 = O & Geo<N>::template dst_mask<DC>();
         if constexpr (STEPS > 1) p2 = p1 & shift<W, S>(p1);
-        if constexpr (STEPS > 2) p4 = p2 & shift<W, 2 * S>(p2);
-        if constexpr (STEPS > 3) p8 = p4 & shift<W, 4 * S>(p4);
+        if constexpr (STEPS > 2 && !R3) p4 = p2 & shift<W, 2 * S>(p2);
+        if constexpr (STEPS > 3 && !R4) p8 = p4 & shift<W, 4 * S>(p4);
     }
     // Extend `t` (opponent squares next to the generator) through the
-    // contiguous opponent run along the direction: runs up to 2^STEPS long.
+    // contiguous opponent run along the direction (runs up to N - 2 long).
     OTH_HD BB<W> fill(BB<W> t) const {
         t = and_or(p1, shift<W, S>(t), t);
         if constexpr (STEPS > 1) t = and_or(p2, shift<W, 2 * S>(t), t);
-        if constexpr (STEPS > 2) t = and_or(p4, shift<W, 4 * S>(t), t);
-        if constexpr (STEPS > 3) t = and_or(p8, shift<W, 8 * S>(t), t);
+        if constexpr (STEPS > 2) {
+            if constexpr (R3) t = and_or(p2, shift<W, 2 * S>(t), t);
+            else t = and_or(p4, shift<W, 4 * S>(t), t);
+        }
+        if constexpr (STEPS > 3) {
+            if constexpr (R4) t = and_or(p4, shift<W, 4 * S>(t), t);
+            else t = and_or(p8, shift<W, 8 * S>(t), t);
+        }
         return t;
     }
     // squares of the run starting one step from the generator g
@@ -320,24 +333,49 @@ template <int N, int S>
 OTH_HD void legal_axis(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& p1, BB<Geo<N>::W>& L) {
     constexpr int W = Geo<N>::W;
     constexpr int STEPS = Pro<N, 0, 1>::STEPS;
+    // The last doubling step may reuse the previous propagator when that still
+    // covers the longest run: 1 + 1 + 2 + 2 = 6 >= N - 2 for N <= 8, and
+    // 1 + 1 + 2 + 4 + 4 = 12 >= N - 2 for N <= 14 (one propagator fewer per axis).
+    constexpr bool R3 = OTH_PROP_REUSE && STEPS == 3 && Geo<N>::MAXRUN <= 6;
+    constexpr bool R4 = OTH_PROP_REUSE && STEPS == 4 && Geo<N>::MAXRUN <= 12;
     BB<W> p2, p4, p8;
     if constexpr (STEPS > 1) p2 = p1 & shift<W, S>(p1);
-    if constexpr (STEPS > 2) p4 = p2 & shift<W, 2 * S>(p2);
-    if constexpr (STEPS > 3) p8 = p4 & shift<W, 4 * S>(p4);
+    if constexpr (STEPS > 2 && !R3) p4 = p2 & shift<W, 2 * S>(p2);
+    if constexpr (STEPS > 3 && !R4) p8 = p4 & shift<W, 4 * S>(p4);
     {  // +S
         BB<W> t = shift<W, S>(P) & p1;
         t |= p1 & shift<W, S>(t);
         if constexpr (STEPS > 1) t |= p2 & shift<W, 2 * S>(t);
-        if constexpr (STEPS > 2) t |= p4 & shift<W, 4 * S>(t);
-        if constexpr (STEPS > 3) t |= p8 & shift<W, 8 * S>(t);
+        if constexpr (STEPS > 2) {
+            if constexpr (R3) t |= p2 & shift<W, 2 * S>(t);
+            else t |= p4 & shift<W, 4 * S>(t);
+        }
+        if constexpr (STEPS > 3) {
+            if constexpr (R4) t |= p4 & shift<W, 4 * S>(t);
+            else t |= p8 & shift<W, 8 * S>(t);
+        }
         L |= shift<W, S>(t);
     }
     {  // -S
         BB<W> t = shift<W, -S>(P) & p1;
         t |= p1 & shift<W, -S>(t);
-        if constexpr (STEPS > 1) t |= shift<W, -S>(p2) & shift<W, -2 * S>(t);
-        if constexpr (STEPS > 2) t |= shift<W, -3 * S>(p4) & shift<W, -4 * S>(t);
-        if constexpr (STEPS > 3) t |= shift<W, -7 * S>(p8) & shift<W, -8 * S>(t);
+        BB<W> p2m, p4m;
+        if constexpr (STEPS > 1) {
+            p2m = shift<W, -S>(p2);
+            t |= p2m & shift<W, -2 * S>(t);
+        }
+        if constexpr (STEPS > 2) {
+            if constexpr (R3) {
+                t |= p2m & shift<W, -2 * S>(t);
+            } else {
+                p4m = shift<W, -3 * S>(p4);
+                t |= p4m & shift<W, -4 * S>(t);
+            }
+        }
+        if constexpr (STEPS > 3) {
+            if constexpr (R4) t |= p4m & shift<W, -4 * S>(t);
+            else t |= shift<W, -7 * S>(p8) & shift<W, -8 * S>(t);
+        }
         L |= shift<W, -S>(t);
     }
 }

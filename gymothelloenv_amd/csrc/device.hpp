@@ -239,19 +239,27 @@ struct Fills {
     template <int S>
     __device__ __forceinline__ static void axis(uint64_t P, uint64_t p1, uint64_t& L, uint64_t& tplus,
                                                 uint64_t& tminus) {
+        // runs are at most N - 2 <= 6 long: the third doubling step reuses p2 (1 + 1 + 2 + 2)
         uint64_t p2 = 0, p4 = 0;
         if constexpr (STEPS > 1) p2 = p1 & (p1 << S);
-        if constexpr (STEPS > 2) p4 = p2 & (p2 << (2 * S));
+        if constexpr (STEPS > 2 && !OTH_PROP_REUSE) p4 = p2 & (p2 << (2 * S));
         uint64_t x = (P << S) & p1;
         x |= p1 & (x << S);
         if constexpr (STEPS > 1) x |= p2 & (x << (2 * S));
-        if constexpr (STEPS > 2) x |= p4 & (x << (4 * S));
+        if constexpr (STEPS > 2) {
+            if constexpr (OTH_PROP_REUSE) x |= p2 & (x << (2 * S));
+            else x |= p4 & (x << (4 * S));
+        }
         tplus = x;
         L |= x << S;
+        const uint64_t p2m = p2 >> S;
         x = (P >> S) & p1;
         x |= p1 & (x >> S);
-        if constexpr (STEPS > 1) x |= (p2 >> S) & (x >> (2 * S));
-        if constexpr (STEPS > 2) x |= (p4 >> (3 * S)) & (x >> (4 * S));
+        if constexpr (STEPS > 1) x |= p2m & (x >> (2 * S));
+        if constexpr (STEPS > 2) {
+            if constexpr (OTH_PROP_REUSE) x |= p2m & (x >> (2 * S));
+            else x |= (p4 >> (3 * S)) & (x >> (4 * S));
+        }
         tminus = x;
         L |= x >> S;
     }
