@@ -432,7 +432,52 @@ OTH_HD BB<Geo<N>::W> flips(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O, const
     return f;
 }
 
+#ifndef OTH_SELECT
+#define OTH_SELECT 2  // 1: six-level binary search; 2: byte prefix counts compared in parallel + nibble table
+#endif
+
+// Position of the j-th set bit (j < popcount) of every 4-bit value v, 2 bits
+// per (v, j) at bit offset 2 * (4 v + j): two 64-bit constants.
+constexpr uint64_t sel4_table(int half) {
+    uint64_t t = 0;
+    for (int v = 8 * half; v < 8 * half + 8; ++v) {
+        int j = 0;
+        for (int b = 0; b < 4; ++b)
+            if ((v >> b) & 1) {
+                t |= (uint64_t)b << (2 * (4 * (v - 8 * half) + j));
+                ++j;
+            }
+    }
+    return t;
+}
+
 // Index of the k-th (0-based, ascending) set bit of a non-zero word, k < popcount.
+#if OTH_SELECT == 2
+// Shallow form for one wave per SIMD: the 32-bit half by the low word's count,
+// the byte by comparing k with the three byte-prefix counts at once, the nibble
+// by one count, the bit from a 128-bit table.
+OTH_HD int select64(uint64_t x, int k) {
+    const uint32_t lo = (uint32_t)x;
+    const int c = popc64(lo);
+    const bool up = k >= c;
+    const uint32_t v = up ? (uint32_t)(x >> 32) : lo;
+    const int kk = up ? k - c : k;
+    const int q1 = popc64(v & 0xFFu), q2 = popc64(v & 0xFFFFu), q3 = popc64(v & 0xFFFFFFu);
+    const bool m1 = q1 <= kk, m2 = q2 <= kk, m3 = q3 <= kk;
+    const int b = (int)m1 + (int)m2 + (int)m3;  // prefix counts grow with the byte index
+    const int qb = m3 ? q3 : (m2 ? q2 : (m1 ? q1 : 0));
+    const uint32_t byte = (v >> (8 * b)) & 0xFFu;
+    const int kb = kk - qb;
+    const int cn = popc64(byte & 0xFu);
+    const bool un = kb >= cn;
+    const uint32_t nib = un ? byte >> 4 : byte & 0xFu;
+    const int kn = un ? kb - cn : kb;
+    constexpr uint64_t T0 = sel4_table(0), T1 = sel4_table(1);
+    const uint64_t t = (nib & 8u) ? T1 : T0;
+    const int bit = (int)((t >> (2 * (4 * (nib & 7u) + kn))) & 3u);
+    return (up ? 32 : 0) + 8 * b + (un ? 4 : 0) + bit;
+}
+#else
 OTH_HD int select64(uint64_t x, int k) {
     int pos = 0;
     uint32_t lo = (uint32_t)x;
@@ -457,6 +502,7 @@ OTH_HD int select64(uint64_t x, int k) {
     }
     return pos;
 }
+#endif
 
 template <int W>
 OTH_HD int select_bit(const BB<W>& b, int k) {

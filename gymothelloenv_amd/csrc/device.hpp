@@ -41,6 +41,9 @@ using namespace oth;
 #ifndef OTH_RAYS
 #define OTH_RAYS 1  // LDS ray-table flips for N <= 8 in k_play
 #endif
+#ifndef OTH_REC_TEMPLATE
+#define OTH_REC_TEMPLATE 1  // k_play specialised for "all per-ply outputs stored" (random / greedy)
+#endif
 #ifndef OTH_BLOCK
 #define OTH_BLOCK 256
 #endif
@@ -696,7 +699,9 @@ __global__ __launch_bounds__(BLOCK) void k_step(uint64_t* __restrict__ boards, u
 // oth_step_policy: `plies` plies of on-device play with the board kept in
 // registers between plies; per-ply outputs stored [ply][E].  Eng::LANES lanes
 // per board (Solo/Rays: 1, Duo: 2); only the pair's leader lane stores.
-template <int N, int POLICY, typename Eng>
+// REC: all three per-ply outputs requested (stores without per-pointer branches,
+// so the ply's tail stays one basic block the scheduler can interleave).
+template <int N, int POLICY, typename Eng, bool REC>
 __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
                                                 uint64_t* __restrict__ legal, int E, uint32_t flags, int plies,
                                                 int32_t* __restrict__ actions, int32_t* __restrict__ rewards,
@@ -755,9 +760,15 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
             }
 #ifndef OTH_ABLATE_NOSTORE
             if (lead) {
-                if (actions) actions[o] = a;
-                if (rewards) rewards[o] = r;
-                if (dones) dones[o] = (uint8_t)d;
+                if constexpr (REC) {
+                    actions[o] = a;
+                    rewards[o] = r;
+                    dones[o] = (uint8_t)d;
+                } else {
+                    if (actions) actions[o] = a;
+                    if (rewards) rewards[o] = r;
+                    if (dones) dones[o] = (uint8_t)d;
+                }
             }
 #endif
         }

@@ -50,31 +50,40 @@ int launch_step(oth_env* env, const int32_t* actions, int32_t* rewards, uint8_t*
     return after_launch("oth_step");
 }
 
+// k_play with the REC specialisation where all per-ply outputs are stored
+// (random / greedy only, to bound the number of maximin instantiations).
+template <int N, int POL, typename Eng>
+void launch_k_play(int lanes_per_board, oth_env* env, int n_plies, int32_t* actions, int32_t* rewards,
+                   uint8_t* dones, uint64_t ply0, hipStream_t st) {
+    const dim3 grid(grid_for((long long)lanes_per_board * env->E)), block(BLOCK);
+    if constexpr (OTH_REC_TEMPLATE && (POL == OTH_POLICY_RANDOM || POL == OTH_POLICY_GREEDY)) {
+        if (actions && rewards && dones) {
+            hipLaunchKernelGGL((k_play<N, POL, Eng, true>), grid, block, 0, st, env->boards, env->meta, env->legal,
+                               env->E, env->flags, n_plies, actions, rewards, dones, env->wdl, rng_of(env), ply0);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((k_play<N, POL, Eng, false>), grid, block, 0, st, env->boards, env->meta, env->legal, env->E,
+                       env->flags, n_plies, actions, rewards, dones, env->wdl, rng_of(env), ply0);
+}
+
 template <int N>
 int launch_play(oth_env* env, int policy, int n_plies, int32_t* actions, int32_t* rewards, uint8_t* dones,
                 uint64_t ply0, hipStream_t st) {
     return with_policy(policy, [&](auto PC) {
         constexpr int POL = decltype(PC)::value;
         if constexpr (Geo<N>::W == 1 && OTH_DUO && POL == OTH_POLICY_RANDOM) {
-            hipLaunchKernelGGL((k_play<N, POL, Duo<N>>), dim3(grid_for(2ll * env->E)), dim3(BLOCK), 0, st,
-                               env->boards, env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards,
-                               dones, env->wdl, rng_of(env), ply0);
+            launch_k_play<N, POL, Duo<N>>(2, env, n_plies, actions, rewards, dones, ply0, st);
         } else if constexpr (Geo<N>::W == 1 && OTH_FILLS &&
                              (POL == OTH_POLICY_RANDOM || (OTH_FILLS_GREEDY && POL == OTH_POLICY_GREEDY))) {
-            hipLaunchKernelGGL((k_play<N, POL, Fills<N>>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards,
-                               env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards, dones, env->wdl,
-                               rng_of(env), ply0);
+            launch_k_play<N, POL, Fills<N>>(1, env, n_plies, actions, rewards, dones, ply0, st);
         } else if constexpr (Geo<N>::W == 1 && OTH_RAYS && POL == OTH_POLICY_RANDOM) {
             // random play with OTH_FILLS=0: ray-table flips with the capping test
             // (greedy keeps Kogge-Stone flips there: the ray tables' exposed LDS
             // latency measured -10 % for greedy without the fills)
-            hipLaunchKernelGGL((k_play<N, POL, Rays<N>>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards,
-                               env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards, dones, env->wdl,
-                               rng_of(env), ply0);
+            launch_k_play<N, POL, Rays<N>>(1, env, n_plies, actions, rewards, dones, ply0, st);
         } else {
-            hipLaunchKernelGGL((k_play<N, POL, Solo<N>>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards,
-                               env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards, dones, env->wdl,
-                               rng_of(env), ply0);
+            launch_k_play<N, POL, Solo<N>>(1, env, n_plies, actions, rewards, dones, ply0, st);
         }
         return after_launch("oth_step_policy");
     });

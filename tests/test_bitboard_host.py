@@ -16,11 +16,15 @@ LIB = os.path.join(HERE, "host", "libbitboard_host.so")
 HDR = os.path.join(os.path.dirname(HERE), "gymothelloenv_amd", "csrc", "bitboard.hpp")
 
 
+def build_host(lib=LIB, defines=()):
+    if not os.path.exists(lib) or os.path.getmtime(lib) < max(os.path.getmtime(SRC), os.path.getmtime(HDR)):
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared"] + list(defines) + ["-o", lib, SRC])
+    return ctypes.CDLL(lib)
+
+
 @pytest.fixture(scope="module")
 def hostlib():
-    if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(SRC), os.path.getmtime(HDR)):
-        subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", LIB, SRC])
-    L = ctypes.CDLL(LIB)
+    L = build_host()
     P = ctypes.c_void_p
     L.host_legal.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P]
     L.host_flips.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P]
@@ -77,6 +81,27 @@ def test_flips_host_build(hostlib, n):
     s.legal[:] = oracle.recompute_legal(s)
     oracle.step(s, 0, sq)
     np.testing.assert_array_equal(out, opp & ~s.boards[:, :W])
+
+
+@pytest.mark.parametrize("variant", [1, 2])
+def test_select_variants_every_rank(variant):
+    """Both select64 forms (OTH_SELECT=1 binary search, 2 byte-parallel), every
+    rank k of dense and sparse (legal-mask-like) words."""
+    L = build_host(os.path.join(HERE, "host", "libbitboard_host_sel%d.so" % variant), ["-DOTH_SELECT=%d" % variant])
+    L.host_select.argtypes = [ctypes.c_uint64, ctypes.c_int]
+    rng = np.random.RandomState(variant)
+    words = [1, 1 << 63, (1 << 64) - 1, 0x8000000000000001, 0x0101010101010101, 0xF0]
+    for _ in range(1500):
+        dens = rng.choice([0.05, 0.15, 0.5, 0.9])
+        x = 0
+        for i in range(64):
+            if rng.rand() < dens:
+                x |= 1 << i
+        words.append(x or (1 << int(rng.randint(64))))
+    for x in words:
+        bits = [i for i in range(64) if (x >> i) & 1]
+        for k, b in enumerate(bits):
+            assert L.host_select(x, k) == b, (hex(x), k)
 
 
 def test_select_and_philox(hostlib):
