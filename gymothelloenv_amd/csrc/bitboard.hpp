@@ -12,6 +12,7 @@
 // log2(N) doubling steps, then one more shift onto an empty square.
 #pragma once
 #include <stdint.h>
+#include <type_traits>
 
 #if defined(__HIPCC__)
 #define OTH_HD __host__ __device__ __forceinline__
@@ -205,6 +206,63 @@ OTH_HD BB<W> shift(const BB<W>& x) {
         return r;
     }
 }
+
+// A one-word board as two dwords.  hipcc splits 64-bit logic into 32-bit halves
+// only after instruction selection, so `(a & b) | c` on uint64_t becomes four
+// VALU ops; on explicit dwords it becomes v_and_or_b32 / gfx950's 3-input
+// v_bitop3_b32 per half.  Constant shifts are one op per half
+// (v_lshlrev_b32 + v_alignbit_b32) instead of a half-rate v_lshlrev_b64.
+struct U2 {
+    uint32_t lo, hi;
+};
+OTH_HD U2 u2(uint64_t v) { return U2{(uint32_t)v, (uint32_t)(v >> 32)}; }
+OTH_HD uint64_t u64(U2 v) { return ((uint64_t)v.hi << 32) | v.lo; }
+OTH_HD U2 operator&(U2 a, U2 b) { return U2{a.lo & b.lo, a.hi & b.hi}; }
+OTH_HD U2 operator|(U2 a, U2 b) { return U2{a.lo | b.lo, a.hi | b.hi}; }
+OTH_HD U2 operator~(U2 a) { return U2{~a.lo, ~a.hi}; }
+OTH_HD U2 operator^(U2 a, U2 b) { return U2{a.lo ^ b.lo, a.hi ^ b.hi}; }
+OTH_HD bool any(U2 a) { return (a.lo | a.hi) != 0u; }
+template <int S>  // S > 0: toward higher squares; S < 0: toward lower squares
+OTH_HD U2 sh(U2 x) {
+    static_assert(S > -64 && S < 64, "shift within one word");
+    if constexpr (S == 0) {
+        return x;
+    } else if constexpr (S >= 32) {
+        return U2{0u, x.lo << (S - 32)};
+    } else if constexpr (S > 0) {
+        return U2{x.lo << S, (x.hi << S) | (x.lo >> (32 - S))};  // v_alignbit_b32
+    } else if constexpr (S <= -32) {
+        return U2{x.hi >> (-S - 32), 0u};
+    } else {
+        return U2{(x.lo >> -S) | (x.hi << (32 + S)), x.hi >> -S};
+    }
+}
+
+// plain 64-bit words with U2's interface (OneWord::greedy runs on either)
+template <int S>
+OTH_HD uint64_t sh(uint64_t x) {
+    static_assert(S > -64 && S < 64, "shift within one word");
+    if constexpr (S >= 0) return x << S;
+    else return x >> -S;
+}
+OTH_HD bool any(uint64_t a) { return a != 0ull; }
+template <typename V>
+OTH_HD V from64(uint64_t v) {
+    if constexpr (std::is_same<V, U2>::value) return u2(v);
+    else return v;
+}
+template <typename V>
+OTH_HD uint64_t to64(V v) {
+    if constexpr (std::is_same<V, U2>::value) return u64(v);
+    else return v;
+}
+
+#ifndef OTH_GREEDY_WORD64
+#define OTH_GREEDY_WORD64 1  // OneWord::greedy on uint64_t (1); dword pairs (0) miscompile inside k_play on gfx950, see DESIGN.md
+#endif
+#ifndef OTH_GREEDY_MASKSEL
+#define OTH_GREEDY_MASKSEL 0  // OneWord::greedy's plane narrowing with mask arithmetic instead of a select
+#endif
 
 template <int N>
 struct Geo {
@@ -432,6 +490,126 @@ OTH_HD BB<Geo<N>::W> flips(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O, const
     return f;
 }
 
+// ---------------------------------------------------------------------------
+// One-word boards (N <= 8) on dword pairs (U2): the legal scan that keeps its
+// per-direction fills, and GreedyPolicy's flip count of every square at once.
+// Ray directions d = 0..7: E, S, SE, SW (toward higher squares), W, N, NW, NE;
+// t[d] = the fill of ray direction d: opponent discs from which an own disc is
+// reached going along d through opponent discs only.  The run a move on square
+// a flips along d is the contiguous part of ray d from a inside t[d].
+template <int N>
+struct OneWord {
+    static_assert(Geo<N>::W == 1, "one-word boards (N <= 8)");
+    static constexpr int STEPS = Pro<N, 0, 1>::STEPS;
+    static_assert(STEPS <= 3 && Geo<N>::MAXRUN <= 6, "1 + 1 + 2 + 2 doubling covers the longest run");
+    static constexpr uint64_t BD = Geo<N>::BOARD.w[0], IN = Geo<N>::INNER.w[0];
+
+    // One axis (+S and -S) of legal_moves for the mover P through the
+    // propagator p1: or-s the squares one step past each fill into L and
+    // returns the fills (tplus: reached stepping +S from an own disc, the
+    // fill of ray direction -S; tminus likewise).  The last doubling step
+    // reuses p2 (runs are at most N - 2 <= 6 long).
+    template <int S>
+    static OTH_HD void axis(U2 P, U2 p1, U2& L, U2& tplus, U2& tminus) {
+        U2 p2{0u, 0u};
+        if constexpr (STEPS > 1) p2 = p1 & sh<S>(p1);
+        U2 x = sh<S>(P) & p1;
+        x = (p1 & sh<S>(x)) | x;
+        if constexpr (STEPS > 1) x = (p2 & sh<2 * S>(x)) | x;
+        if constexpr (STEPS > 2) x = (p2 & sh<2 * S>(x)) | x;
+        tplus = x;
+        L = L | sh<S>(x);
+        const U2 p2m = sh<-S>(p2);
+        x = sh<-S>(P) & p1;
+        x = (p1 & sh<-S>(x)) | x;
+        if constexpr (STEPS > 1) x = (p2m & sh<-2 * S>(x)) | x;
+        if constexpr (STEPS > 2) x = (p2m & sh<-2 * S>(x)) | x;
+        tminus = x;
+        L = L | sh<-S>(x);
+    }
+    // get_possible_actions (othello.py:313-343) for the mover P against O,
+    // with the eight fills stored in t.
+    static OTH_HD uint64_t legal(uint64_t Pw, uint64_t Ow, uint64_t t[8]) {
+        const U2 P = u2(Pw), O = u2(Ow), pin = O & u2(IN);
+        U2 L{0u, 0u}, f[8];
+        axis<1>(P, pin, L, f[4], f[0]);
+        axis<N>(P, O, L, f[5], f[1]);
+        axis<N + 1>(P, pin, L, f[6], f[2]);
+        axis<N - 1>(P, pin, L, f[7], f[3]);
+#pragma unroll
+        for (int d = 0; d < 8; ++d) t[d] = u64(f[d]);
+        return u64(L & ~(P | O) & u2(BD));
+    }
+
+    // Run length along one ray direction (step S) for every square, as a
+    // 3-bit number on bit planes: A_j = {a : a + S, ..., a + jS all in T}
+    // from doubling shifts; the nested A_1..A_6 count in binary as
+    // (A1^..^A6, (A2^A4)|A6, A4).  No wrap-around masks: the horizontal and
+    // diagonal fills hold no edge-column square, and every A_j lies in A_1.
+    template <int S, typename V>
+    static OTH_HD void run_len(V T, V out[3]) {
+        constexpr int R = N - 2;
+        const V z = from64<V>(0ull);
+        const V A1 = sh<-S>(T);
+        V A2 = z, A3 = z, A4 = z, A5 = z, A6 = z;
+        if constexpr (R >= 2) A2 = A1 & sh<-S>(A1);
+        if constexpr (R >= 3) A3 = A2 & sh<-2 * S>(A1);
+        if constexpr (R >= 4) A4 = A2 & sh<-2 * S>(A2);
+        if constexpr (R >= 5) A5 = A4 & sh<-4 * S>(A1);
+        if constexpr (R >= 6) A6 = A4 & sh<-4 * S>(A2);
+        out[0] = A1 ^ A2 ^ A3 ^ A4 ^ A5 ^ A6;
+        out[1] = (A2 ^ A4) | A6;
+        out[2] = A4;
+    }
+    // out[0..NO) = a[0..NA) + b[0..NB) on bit planes (ripple carry, carries past NO dropped)
+    template <int NA, int NB, int NO, typename V>
+    static OTH_HD void add_planes(const V* a, const V* b, V* out) {
+        const V z = from64<V>(0ull);
+        V c = z;
+#pragma unroll
+        for (int i = 0; i < NO; ++i) {
+            const V x = i < NA ? a[i] : z, y = i < NB ? b[i] : z;
+            out[i] = x ^ y ^ c;
+            c = (x & y) | (c & (x | y));
+        }
+    }
+    // GreedyPolicy.get_action (simple_policies.py:69-92): the candidate (a
+    // square of `legal`) flipping the most discs, the lowest of equal counts
+    // (np.argmax); -1 without candidates.  The eight run lengths are summed on
+    // bit planes (at most 19 flips on a board of N <= 8: 5 planes), then the
+    // largest total among the candidates is found plane by plane from the top.
+    static OTH_HD int greedy(const uint64_t t[8], uint64_t legal) {
+        using V = typename std::conditional<OTH_GREEDY_WORD64 != 0, uint64_t, U2>::type;
+        V n[8][3];
+        run_len<1>(from64<V>(t[0]), n[0]);
+        run_len<N>(from64<V>(t[1]), n[1]);
+        run_len<N + 1>(from64<V>(t[2]), n[2]);
+        run_len<N - 1>(from64<V>(t[3]), n[3]);
+        run_len<-1>(from64<V>(t[4]), n[4]);
+        run_len<-N>(from64<V>(t[5]), n[5]);
+        run_len<-N - 1>(from64<V>(t[6]), n[6]);
+        run_len<-N + 1>(from64<V>(t[7]), n[7]);
+        V s4[4][4], s5[2][5], tot[5];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) add_planes<3, 3, 4>(n[2 * i], n[2 * i + 1], s4[i]);
+        add_planes<4, 4, 5>(s4[0], s4[1], s5[0]);
+        add_planes<4, 4, 5>(s4[2], s4[3], s5[1]);
+        add_planes<5, 5, 5>(s5[0], s5[1], tot);
+        uint64_t cand = legal;
+#pragma unroll
+        for (int i = 4; i >= 0; --i) {
+            const uint64_t h = cand & to64(tot[i]);
+#if OTH_GREEDY_MASKSEL
+            const uint64_t keep = (uint64_t)(h == 0ull) - 1ull;  // all ones when h != 0
+            cand = (h & keep) | (cand & ~keep);
+#else
+            cand = h ? h : cand;
+#endif
+        }
+        return cand ? __builtin_ctzll(cand) : -1;
+    }
+};
+
 #ifndef OTH_SELECT
 #define OTH_SELECT 2  // 1: six-level binary search; 2: byte prefix counts compared in parallel + nibble table
 #endif
@@ -506,6 +684,10 @@ OTH_HD int select64(uint64_t x, int k) {
 
 template <int W>
 OTH_HD int select_bit(const BB<W>& b, int k) {
+    if constexpr (W == 1) {  // branch-free: -1 when k >= popcount (no legal move)
+        const int s = select64(b.w[0], k);
+        return k < popc64(b.w[0]) ? s : -1;
+    }
     int res = -1;
     bool found = false;
 #pragma unroll

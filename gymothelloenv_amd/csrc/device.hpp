@@ -47,6 +47,18 @@ using namespace oth;
 #ifndef OTH_BLOCK
 #define OTH_BLOCK 256
 #endif
+#ifndef OTH_U32
+#define OTH_U32 1  // Fills engine scans on dword pairs (bitboard.hpp U2)
+#endif
+#ifndef OTH_GREEDY_PLANES
+#define OTH_GREEDY_PLANES 1  // GreedyPolicy on bit planes for N <= 8 (bitboard.hpp OneWord::greedy)
+#endif
+#ifndef OTH_PICKED
+#define OTH_PICKED 1  // k_play: the action is a pick from the legal mask, flips without a validity branch
+#endif
+#ifndef OTH_DRAW_ROTATE
+#define OTH_DRAW_ROTATE 1  // k_play random: rotate the 4-word Philox block per ply instead of picking word g % 4
+#endif
 
 namespace oth_dev {
 
@@ -269,6 +281,14 @@ struct Fills {
     // get_possible_actions for mover P (legal_moves' axis-paired scan), keeping the fills
     __device__ __forceinline__ BB<1> legal(const BB<1>& Pb, const BB<1>& Ob) const {
         static_assert(Pro<N, 0, 1>::STEPS <= 3, "N <= 8");
+#if OTH_U32
+        // the same scan on dwords (bitboard.hpp OneWord): v_bitop3 / v_and_or
+        // instead of and + or pairs, 32-bit shifts instead of v_lshl*_b64
+        static_assert(OTH_PROP_REUSE, "dword scan assumes the reused last propagator");
+        BB<1> r;
+        r.w[0] = OneWord<N>::legal(Pb.w[0], Ob.w[0], t);
+        return r;
+#else
         const uint64_t P = Pb.w[0], O = Ob.w[0], pin = O & IN;
         uint64_t L = 0;
         axis<1>(P, pin, L, t[4], t[0]);          // W uses +1 fill, E uses -1 fill
@@ -278,6 +298,7 @@ struct Fills {
         BB<1> r;
         r.w[0] = L & ~(P | O) & BD;
         return r;
+#endif
     }
     __device__ __forceinline__ BB<1> flip(const BB<1>&, const BB<1>&, int a) const {
         const uint64_t* r = rays + a;
@@ -300,6 +321,8 @@ struct Fills {
         out.w[0] = f;
         return out;
     }
+    // GreedyPolicy from the fills of the side to move (bitboard.hpp OneWord::greedy)
+    __device__ __forceinline__ int greedy(const BB<1>& legal) const { return OneWord<N>::greedy(t, legal.w[0]); }
     // recompute the fills for the side to move (after a load or a reset)
     __device__ __forceinline__ void prime(const Lane<N>& s) const {
         const bool tw = (s.meta & M_TURN_WHITE) != 0;
@@ -404,33 +427,15 @@ __device__ __forceinline__ void reset_lane(Lane<N>& s, uint64_t seed, uint32_t i
     s.meta = (rl & 0xffu) << M_RAND_SHIFT;
 }
 
-// OthelloBaseEnv.step (othello.py:412-462) for one lane.  Returns the winner
-// code (0 none) through `winner` when the game ends on this ply.
+// The rest of OthelloBaseEnv.step after update_board (othello.py:425-462):
+// full board / sudden death, the opponent's legal moves, pass and double pass,
+// winner and reward.  P / O are the mover's / opponent's discs after the move.
 template <int N, typename Eng>
-__device__ __forceinline__ void step_lane(Lane<N>& s, int a, uint32_t flags, int& reward, int& done, int& winner,
-                                          const Eng& eng) {
+__device__ __forceinline__ void finish_step(Lane<N>& s, bool tw, bool valid, const BB<Geo<N>::W>& P,
+                                            const BB<Geo<N>::W>& O, uint32_t flags, int& reward, int& done,
+                                            int& winner, const Eng& eng) {
     constexpr int W = Geo<N>::W;
     constexpr int NN = N * N;
-    winner = NO_DISK;
-    if (s.meta & M_TERMINATED) {  // reference: ValueError (othello.py:415-416)
-        reward = 0;
-        done = 1;
-        return;
-    }
-    const bool tw = (s.meta & M_TURN_WHITE) != 0;
-    BB<W> P = tw ? s.white : s.black;
-    BB<W> O = tw ? s.black : s.white;
-    const bool valid = a >= 0 && a < NN && test(s.legal, a);  // `action not in possible_moves` (:417)
-    if (valid) {                                               // update_board (:391-410)
-        const BB<W> m = square<W>(a);
-#ifdef OTH_ABLATE_NOFLIP  // timing ablation only
-        const BB<W> f = zero<W>();
-#else
-        const BB<W> f = eng.flip(P, O, a);
-#endif
-        P |= f | m;
-        O = O & ~(f | m);
-    }
     const bool full = !any(~(P | O) & Geo<N>::BOARD);                       // :425-426
     const bool sudden = !valid && (flags & OTH_SUDDEN_DEATH);              // :427
     const int pc = popcount(P), oc = popcount(O);
@@ -475,6 +480,52 @@ __device__ __forceinline__ void step_lane(Lane<N>& s, int a, uint32_t flags, int
              (term ? (wcode << M_WINNER_SHIFT) : 0u);
     reward = r;
     done = term ? 1 : 0;
+}
+
+// OthelloBaseEnv.step (othello.py:412-462) for one lane.  Returns the winner
+// code (0 none) through `winner` when the game ends on this ply.
+// PICKED: `a` is a policy's pick from s.legal, or -1 when s.legal is empty, so
+// validity is a >= 0 and the flip is computed without a branch and masked.
+template <int N, typename Eng, bool PICKED = false>
+__device__ __forceinline__ void step_lane(Lane<N>& s, int a, uint32_t flags, int& reward, int& done, int& winner,
+                                          const Eng& eng) {
+    constexpr int W = Geo<N>::W;
+    constexpr int NN = N * N;
+    winner = NO_DISK;
+    if (s.meta & M_TERMINATED) {  // reference: ValueError (othello.py:415-416)
+        reward = 0;
+        done = 1;
+        return;
+    }
+    const bool tw = (s.meta & M_TURN_WHITE) != 0;
+    BB<W> P = tw ? s.white : s.black;
+    BB<W> O = tw ? s.black : s.white;
+    if constexpr (PICKED && Eng::RAY_WORDS > 0) {
+        static_assert(W == 1, "ray engines are one-word");
+        const bool valid = a >= 0;
+        const uint64_t m = valid ? 1ull << (a & 63) : 0ull;
+#ifdef OTH_ABLATE_NOFLIP  // timing ablation only
+        const uint64_t f = 0;
+#else
+        const uint64_t f = eng.flip(P, O, a & 63).w[0] & (0ull - (uint64_t)valid);
+#endif
+        P.w[0] |= f | m;
+        O.w[0] &= ~(f | m);
+        finish_step<N>(s, tw, valid, P, O, flags, reward, done, winner, eng);
+        return;
+    }
+    const bool valid = a >= 0 && a < NN && test(s.legal, a);  // `action not in possible_moves` (:417)
+    if (valid) {                                               // update_board (:391-410)
+        const BB<W> m = square<W>(a);
+#ifdef OTH_ABLATE_NOFLIP  // timing ablation only
+        const BB<W> f = zero<W>();
+#else
+        const BB<W> f = eng.flip(P, O, a);
+#endif
+        P |= f | m;
+        O = O & ~(f | m);
+    }
+    finish_step<N>(s, tw, valid, P, O, flags, reward, done, winner, eng);
 }
 
 // RandomPolicy.get_action (simple_policies.py:37-41): possible_moves[randint(len)]
@@ -526,6 +577,17 @@ __device__ __forceinline__ void greedy_scan(const Lane<N>& s, int parity, int st
 template <int N, typename Eng>
 __device__ __forceinline__ int greedy_action(const Lane<N>& s, const Eng& eng) {
     static_assert(Eng::LANES == 1, "greedy runs one lane per board");
+#if OTH_GREEDY_PLANES
+    // every square's flip count on bit planes, no loop over the candidates
+    if constexpr (std::is_same<Eng, Fills<N>>::value) {
+        return eng.greedy(s.legal);  // the fills of the side to move are carried from the last scan
+    } else if constexpr (Geo<N>::W == 1) {
+        const bool tw = (s.meta & M_TURN_WHITE) != 0;
+        uint64_t t[8];
+        (void)OneWord<N>::legal(tw ? s.white.w[0] : s.black.w[0], tw ? s.black.w[0] : s.white.w[0], t);
+        return OneWord<N>::greedy(t, s.legal.w[0]);
+    }
+#endif
     int best, cnt;
     greedy_scan<N>(s, 0, 1, best, cnt, eng);
     return best;
@@ -720,6 +782,9 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
         load_lane<N>(s, boards, meta, legal, e);
         eng.prime(s);
         U4 draws{0, 0, 0, 0};
+        int32_t* act_p = actions + e;
+        int32_t* rew_p = rewards + e;
+        uint8_t* done_p = dones + e;
         for (int p = 0; p < plies; ++p) {
             const uint64_t g = ply0 + (uint64_t)p;
             const size_t o = (size_t)p * (size_t)E + (size_t)e;
@@ -730,13 +795,20 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
                 draws = U4{h, h * 3u, h * 5u, h * 7u};
             }
 #else
-            if (POLICY == OTH_POLICY_RANDOM && (p == 0 || (g & 3) == 0)) draws = philox4(rng.seed, id, g >> 2, RNG_ACTION);
+            if (POLICY == OTH_POLICY_RANDOM && (p == 0 || (g & 3) == 0)) {
+                draws = philox4(rng.seed, id, g >> 2, RNG_ACTION);
+#if OTH_DRAW_ROTATE
+                // draws.x is always this ply's word: rotate to word g % 4 at the launch's first ply
+                if (p == 0)
+                    for (uint32_t j = 0; j < (uint32_t)(g & 3); ++j) draws = U4{draws.y, draws.z, draws.w, draws.x};
+#endif
+            }
 #endif
             int a = -1, r = 0, d = 1, win = NO_DISK;
             if (!(s.meta & M_TERMINATED)) {
                 const uint32_t rl = s.meta >> M_RAND_SHIFT;
                 if (POLICY == OTH_POLICY_RANDOM || rl > 0) {
-                    const uint32_t u = POLICY == OTH_POLICY_RANDOM ? pick4(draws, (uint32_t)(g & 3))
+                    const uint32_t u = POLICY == OTH_POLICY_RANDOM ? (OTH_DRAW_ROTATE ? draws.x : pick4(draws, (uint32_t)(g & 3)))
                                                                    : action_draw(rng.seed, id, g);
 #ifdef OTH_ABLATE_SELECT  // timing ablation only: lowest legal square
                     a = __builtin_ctzll(s.legal.w[0] | (1ull << 63)) + (int)(u & 0);
@@ -747,7 +819,7 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
                 } else {
                     a = policy_action<N, POLICY>(s, eng);
                 }
-                step_lane<N>(s, a, flags, r, d, win, eng);
+                step_lane<N, Eng, (bool)OTH_PICKED>(s, a, flags, r, d, win, eng);  // a: a pick from s.legal
                 if (d) {
                     cb += win == BLACK_DISK;
                     cd += win == NO_DISK;
@@ -758,12 +830,16 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
                     }
                 }
             }
+            if (POLICY == OTH_POLICY_RANDOM && OTH_DRAW_ROTATE) draws = U4{draws.y, draws.z, draws.w, draws.x};
 #ifndef OTH_ABLATE_NOSTORE
             if (lead) {
-                if constexpr (REC) {
-                    actions[o] = a;
-                    rewards[o] = r;
-                    dones[o] = (uint8_t)d;
+                if constexpr (REC) {  // running pointers: one 64-bit add each per ply
+                    *act_p = a;
+                    *rew_p = r;
+                    *done_p = (uint8_t)d;
+                    act_p += E;
+                    rew_p += E;
+                    done_p += E;
                 } else {
                     if (actions) actions[o] = a;
                     if (rewards) rewards[o] = r;

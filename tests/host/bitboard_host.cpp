@@ -1,5 +1,6 @@
 // Host build of csrc/bitboard.hpp (the same templates the kernels use) for CPU
-// tests: legal_moves<N> / flips<N> / select_bit / philox4 exported with C linkage.
+// tests: legal_moves<N> / flips<N> / select_bit / philox4 and the one-word
+// fills scan + bit-plane greedy (OneWord<N>) exported with C linkage.
 // Built by tests/test_bitboard_host.py with g++; test infrastructure only.
 #include <stdint.h>
 #include <string.h>
@@ -36,6 +37,30 @@ static void flips_n(int E, const uint64_t* mover, const uint64_t* opp, const int
     }
 }
 
+template <int N>
+static void legal_fills_n(int E, const uint64_t* mover, const uint64_t* opp, uint64_t* out, uint64_t* fills) {
+    for (int e = 0; e < E; ++e) out[e] = OneWord<N>::legal(mover[e], opp[e], fills + 8 * e);
+}
+
+template <int N>
+static void greedy_planes_n(int E, const uint64_t* mover, const uint64_t* opp, const uint64_t* legal, int32_t* out) {
+    for (int e = 0; e < E; ++e) {
+        uint64_t t[8];
+        (void)OneWord<N>::legal(mover[e], opp[e], t);
+        out[e] = OneWord<N>::greedy(t, legal[e]);
+    }
+}
+
+#define DISPATCH8(fn, ...)                 \
+    switch (n) {                           \
+        case 4: fn<4>(__VA_ARGS__); break; \
+        case 5: fn<5>(__VA_ARGS__); break; \
+        case 6: fn<6>(__VA_ARGS__); break; \
+        case 7: fn<7>(__VA_ARGS__); break; \
+        case 8: fn<8>(__VA_ARGS__); break; \
+        default: return -1;                \
+    }
+
 #define DISPATCH(fn, ...)                \
     switch (n) {                         \
         case 4: fn<4>(__VA_ARGS__); break;   \
@@ -61,6 +86,14 @@ int host_legal(int n, int E, const uint64_t* mover, const uint64_t* opp, uint64_
 }
 int host_flips(int n, int E, const uint64_t* mover, const uint64_t* opp, const int32_t* sq, uint64_t* out) {
     DISPATCH(flips_n, E, mover, opp, sq, out);
+    return 0;
+}
+int host_legal_fills(int n, int E, const uint64_t* mover, const uint64_t* opp, uint64_t* out, uint64_t* fills) {
+    DISPATCH8(legal_fills_n, E, mover, opp, out, fills);
+    return 0;
+}
+int host_greedy_planes(int n, int E, const uint64_t* mover, const uint64_t* opp, const uint64_t* legal, int32_t* out) {
+    DISPATCH8(greedy_planes_n, E, mover, opp, legal, out);
     return 0;
 }
 int host_select(uint64_t x, int k) { return select64(x, k); }

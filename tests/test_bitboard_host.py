@@ -29,6 +29,8 @@ def hostlib():
     L.host_legal.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P]
     L.host_flips.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P]
     L.host_select.argtypes = [ctypes.c_uint64, ctypes.c_int]
+    L.host_legal_fills.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P]
+    L.host_greedy_planes.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P]
     L.host_philox4.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32, P]
     return L
 
@@ -102,6 +104,56 @@ def test_select_variants_every_rank(variant):
         bits = [i for i in range(64) if (x >> i) & 1]
         for k, b in enumerate(bits):
             assert L.host_select(x, k) == b, (hex(x), k)
+
+
+RAY_DIRS = [(0, 1), (1, 0), (1, 1), (1, -1), (0, -1), (-1, 0), (-1, -1), (-1, 1)]  # E S SE SW W N NW NE
+
+
+@pytest.mark.parametrize("n", [4, 5, 6, 7, 8])
+def test_dword_scan_and_fills_host_build(hostlib, n):
+    """OneWord<N>::legal (the fills engine's dword-pair scan) == the oracle's
+    legal moves; and the fills carry update_board: from every legal square the
+    discs flipped (flips<N>) are exactly the contiguous run of each ray inside
+    that ray direction's fill."""
+    rng = np.random.RandomState(100 + n)
+    for density in (0.3, 0.6, 0.9):
+        _, mover, opp = random_boards(n, 1500, rng, density)
+        out = np.zeros_like(mover)
+        fills = np.zeros((len(mover), 8), dtype=np.uint64)
+        assert hostlib.host_legal_fills(n, len(mover), ptr(mover), ptr(opp), ptr(out), ptr(fills)) == 0
+        np.testing.assert_array_equal(out, oracle.legal(n, mover, opp))
+        for e in range(0, len(mover), 5):
+            lg = int(out[e, 0])
+            for a in (b for b in range(n * n) if (lg >> b) & 1):
+                f = np.zeros((1, 1), dtype=np.uint64)
+                hostlib.host_flips(n, 1, ptr(mover[e:e + 1].copy()), ptr(opp[e:e + 1].copy()),
+                                   ptr(np.array([a], dtype=np.int32)), ptr(f))
+                runs = 0
+                for d, (dr, dc) in enumerate(RAY_DIRS):
+                    r, c = divmod(a, n)
+                    r, c = r + dr, c + dc
+                    while 0 <= r < n and 0 <= c < n and (int(fills[e, d]) >> (r * n + c)) & 1:
+                        runs |= 1 << (r * n + c)
+                        r, c = r + dr, c + dc
+                assert runs == int(f[0, 0]), (n, e, a)
+
+
+@pytest.mark.parametrize("n", [4, 5, 6, 7, 8])
+def test_greedy_planes_host_build(hostlib, n):
+    """OneWord<N>::greedy (every square's flip count on bit planes) plays the
+    oracle's GreedyPolicy move (one simulated step per candidate,
+    simple_policies.py:69-92), incl. the lowest-square tie-break and -1 when
+    the mover has no move."""
+    rng = np.random.RandomState(200 + n)
+    for density in (0.3, 0.6, 0.85, 0.97):
+        _, mover, opp = random_boards(n, 3000, rng, density)
+        s = oracle.State(n, len(mover))
+        s.boards[:] = np.concatenate([mover, opp], axis=1)  # black = mover, black to move
+        s.meta[:] = oracle.meta_from(-np.ones(len(mover)))
+        s.legal[:] = oracle.recompute_legal(s)
+        out = np.zeros(len(mover), dtype=np.int32)
+        assert hostlib.host_greedy_planes(n, len(mover), ptr(mover), ptr(opp), ptr(s.legal), ptr(out)) == 0
+        np.testing.assert_array_equal(out, oracle.greedy(s))
 
 
 def test_select_and_philox(hostlib):

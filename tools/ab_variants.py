@@ -27,14 +27,17 @@ def build(specs):
         hb.build(force=True, extra_flags=flags.split(), out=os.path.join(VDIR, "liboth_%s.so" % name))
 
 
-def run(names, E, n, plies, launches, rounds, policy, check=True):
+def run(names, E, n, plies, launches, rounds, policy, check=True, init_rand=0):
     import torch
 
     from gymothelloenv_amd import _lib as L
     from gymothelloenv_amd.vec_env import VecOthelloEnv
     libs = {nm: L.load_path(os.path.join(VDIR, "liboth_%s.so" % nm)) for nm in names}
-    envs = {nm: VecOthelloEnv(E, board_size=n, auto_reset=True, seed=0, device="cuda:0", lib=lib)
+    envs = {nm: VecOthelloEnv(E, board_size=n, auto_reset=True, seed=0, device="cuda:0", lib=lib,
+                             initial_rand_steps=init_rand)
             for nm, lib in libs.items()}
+    for env in envs.values():
+        env.reset()
     # correctness: identical trajectories
     ref = None
     for nm, env in envs.items():
@@ -82,12 +85,14 @@ def main():
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--policy", default="random")
+    ap.add_argument("--init-rand", type=int, default=0, help="random-opening bound (initial_rand_steps)")
     ap.add_argument("--no-check", action="store_true", help="timing ablations: outputs differ by design")
     a = ap.parse_args()
     if a.build:
         build(a.build)
     if a.run:
-        run(a.run, a.envs, a.board_size, a.plies, a.launches, a.rounds, a.policy, check=not a.no_check)
+        run(a.run, a.envs, a.board_size, a.plies, a.launches, a.rounds, a.policy, check=not a.no_check,
+            init_rand=a.init_rand)
 
 
 if __name__ == "__main__":
