@@ -1088,4 +1088,96 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const uint64_t* __restrict__ 
     }
 }
 
+// Quad kernel for N*N % 4 == 0 (even N): one thread writes 4 consecutive
+// squares of one plane as one vector store (16 B for f32 / i32, 4 B for i8,
+// 2 x 16 B for the 8-byte types), so a wave writes 64 contiguous quads -- the
+// whole (planes, N, N) block of 1 to 4 boards.  The board words are read by
+// the wave's lanes of one board at once (broadcast loads).  Same values as
+// k_observe: LAYOUT / T are template parameters, so the only index math is
+// division by compile-time constants.
+template <typename T>
+struct Quad {
+    T v[4];
+};
+template <typename T>
+__device__ __forceinline__ void put_quad(T* out, uint32_t q, int v0, int v1, int v2, int v3) {
+    if constexpr (sizeof(T) == 1) {
+        const uint32_t x = (uint32_t)(uint8_t)(int8_t)v0 | ((uint32_t)(uint8_t)(int8_t)v1 << 8) |
+                           ((uint32_t)(uint8_t)(int8_t)v2 << 16) | ((uint32_t)(uint8_t)(int8_t)v3 << 24);
+        reinterpret_cast<uint32_t*>(out)[q] = x;
+    } else if constexpr (sizeof(T) == 4) {
+        using V4 = typename std::conditional<std::is_same<T, float>::value, float4, int4>::type;
+        V4 x;
+        x.x = (T)v0;
+        x.y = (T)v1;
+        x.z = (T)v2;
+        x.w = (T)v3;
+        reinterpret_cast<V4*>(out)[q] = x;
+    } else {
+        using V2 = typename std::conditional<std::is_same<T, double>::value, double2, longlong2>::type;
+        V2 a, b;
+        a.x = (T)v0;
+        a.y = (T)v1;
+        b.x = (T)v2;
+        b.y = (T)v3;
+        reinterpret_cast<V2*>(out)[2 * (size_t)q] = a;
+        reinterpret_cast<V2*>(out)[2 * (size_t)q + 1] = b;
+    }
+}
+
+template <int N, int LAYOUT, typename T>
+__global__ __launch_bounds__(BLOCK) void k_observe_q(const uint64_t* __restrict__ boards,
+                                                     const uint16_t* __restrict__ meta,
+                                                     const uint64_t* __restrict__ legal, uint32_t total_quads,
+                                                     T* __restrict__ out) {
+    constexpr int W = Geo<N>::W;
+    constexpr int NN = N * N;
+    static_assert(NN % 4 == 0, "quads of squares");
+    constexpr uint32_t Q = NN / 4;
+    constexpr uint32_t PLANES = LAYOUT == OTH_OBS_BOARD_LEGAL ? 2 : (LAYOUT == OTH_OBS_MAKE_STATE ? 4 : 1);
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < total_quads; i += gridDim.x * BLOCK) {
+        const uint32_t q = i % Q;
+        const uint32_t rest = i / Q;
+        const uint32_t plane = rest % PLANES;
+        const uint32_t e = rest / PLANES;
+        const int a0 = 4 * (int)q, wi = a0 / 64, bi = a0 % 64;  // 4 | 64: a quad never straddles words
+        const uint32_t nb = (uint32_t)(boards[(size_t)e * 2 * W + wi] >> bi) & 0xFu;
+        const uint32_t nw = (uint32_t)(boards[(size_t)e * 2 * W + W + wi] >> bi) & 0xFu;
+        int v[4];
+        if constexpr (LAYOUT == OTH_OBS_ABSOLUTE) {  // othello.py:257
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = (int)((nw >> j) & 1u) - (int)((nb >> j) & 1u);
+        } else if constexpr (LAYOUT == OTH_OBS_MAKE_STATE) {  // util.py:48-74
+            const bool tw = (meta[e] & M_TURN_WHITE) != 0;
+            uint32_t bits = 0;
+            if (plane == 0) {
+                bits = nb;
+            } else if (plane == 1) {
+                bits = nw;
+            } else if (plane == 2) {
+                bits = tw ? 0xFu : 0u;
+            } else {  // util.py:55: the legal plane only when >= 2 moves
+                int cnt = 0;
+#pragma unroll
+                for (int k = 0; k < W; ++k) cnt += popc64(legal[(size_t)e * W + k]);
+                bits = cnt > 1 ? (uint32_t)(legal[(size_t)e * W + wi] >> bi) & 0xFu : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = (int)((bits >> j) & 1u);
+        } else {  // othello.py:363-376: mover +1, opponent -1; plane 1 the legal squares
+            if (plane == 0) {
+                const bool tw = (meta[e] & M_TURN_WHITE) != 0;
+                const uint32_t mv = tw ? nw : nb, op = tw ? nb : nw;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = (int)((mv >> j) & 1u) - (int)((op >> j) & 1u);
+            } else {
+                const uint32_t nl = (uint32_t)(legal[(size_t)e * W + wi] >> bi) & 0xFu;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = (int)((nl >> j) & 1u);
+            }
+        }
+        put_quad<T>(out, i, v[0], v[1], v[2], v[3]);
+    }
+}
+
 }  // namespace oth_dev

@@ -129,10 +129,55 @@ int launch_legal_moves(int n, const uint64_t* mover, const uint64_t* opp, uint64
     return after_launch("oth_legal_moves");
 }
 
+#ifndef OTH_OBS_QUADS
+#define OTH_OBS_QUADS 1  // k_observe_q (vector stores of 4 squares) where N*N % 4 == 0
+#endif
+
+template <int N, typename T>
+void launch_observe_q(oth_env* env, int layout, uint32_t quads, void* out, hipStream_t st) {
+    int grid = grid_for(quads);
+    if (grid > (1 << 20)) grid = 1 << 20;
+    T* o = static_cast<T*>(out);
+    switch (layout) {
+        case OTH_OBS_BOARD:
+            hipLaunchKernelGGL((k_observe_q<N, OTH_OBS_BOARD, T>), dim3(grid), dim3(BLOCK), 0, st, env->boards,
+                               env->meta, env->legal, quads, o);
+            break;
+        case OTH_OBS_BOARD_LEGAL:
+            hipLaunchKernelGGL((k_observe_q<N, OTH_OBS_BOARD_LEGAL, T>), dim3(grid), dim3(BLOCK), 0, st, env->boards,
+                               env->meta, env->legal, quads, o);
+            break;
+        case OTH_OBS_MAKE_STATE:
+            hipLaunchKernelGGL((k_observe_q<N, OTH_OBS_MAKE_STATE, T>), dim3(grid), dim3(BLOCK), 0, st, env->boards,
+                               env->meta, env->legal, quads, o);
+            break;
+        default:
+            hipLaunchKernelGGL((k_observe_q<N, OTH_OBS_ABSOLUTE, T>), dim3(grid), dim3(BLOCK), 0, st, env->boards,
+                               env->meta, env->legal, quads, o);
+            break;
+    }
+}
+
 template <int N>
 int launch_observe(oth_env* env, int layout, int dtype, void* out, hipStream_t st) {
     const int planes = layout == OTH_OBS_BOARD_LEGAL ? 2 : (layout == OTH_OBS_MAKE_STATE ? 4 : 1);
     const long long total = (long long)env->E * planes * N * N;
+    static const int esize[5] = {1, 4, 8, 4, 8};
+    if constexpr ((N * N) % 4 == 0 && OTH_OBS_QUADS) {
+        // vector stores need a 4-element-aligned base and 32-bit quad indices
+        if (dtype >= OTH_I8 && dtype <= OTH_F64 && (uintptr_t)out % (4 * esize[dtype]) == 0 &&
+            total / 4 < (1ll << 31)) {
+            const uint32_t quads = (uint32_t)(total / 4);
+            switch (dtype) {
+                case OTH_I8: launch_observe_q<N, int8_t>(env, layout, quads, out, st); break;
+                case OTH_I32: launch_observe_q<N, int32_t>(env, layout, quads, out, st); break;
+                case OTH_I64: launch_observe_q<N, long long>(env, layout, quads, out, st); break;
+                case OTH_F32: launch_observe_q<N, float>(env, layout, quads, out, st); break;
+                default: launch_observe_q<N, double>(env, layout, quads, out, st); break;
+            }
+            return after_launch("oth_observe");
+        }
+    }
     int grid = grid_for(total);
     if (grid > 65536) grid = 65536;
     hipLaunchKernelGGL(k_observe<N>, dim3(grid), dim3(BLOCK), 0, st, env->boards, env->meta, env->legal, env->E,

@@ -441,3 +441,47 @@ def test_vs_maximin_opponent_on_oracle(torch_cuda):
         np.testing.assert_array_equal(plies.cpu().numpy(), opl)
     b, m, lg = get_state_np(env)
     np.testing.assert_array_equal(b, s.boards)
+
+
+def _obs_np(n, boards, meta, legal, layout):
+    """numpy restatement of get_observation / make_state / board_state for the
+    observation kernels (othello.py:257,363-376; util.py:48-74)."""
+    W = oracle.nwords(n)
+    sq = np.arange(n * n)
+
+    def bits(words):
+        return ((words[:, sq // 64] >> (sq % 64).astype(np.uint64)) & np.uint64(1)).astype(np.int64)
+
+    b, w, lg = bits(boards[:, :W]), bits(boards[:, W:]), bits(legal)
+    tw = (meta.astype(np.int64) & 1).astype(bool)[:, None]
+    E = len(meta)
+    if layout == "absolute":
+        return (w - b).reshape(E, n, n)
+    mover = np.where(tw, w - b, b - w)
+    if layout == "board":
+        return mover.reshape(E, n, n)
+    if layout == "board_legal":
+        return np.stack([mover, lg], 1).reshape(E, 2, n, n)
+    ms_legal = np.where(lg.sum(1, keepdims=True) > 1, lg, 0)
+    return np.stack([b, w, np.broadcast_to(tw.astype(np.int64), b.shape), ms_legal], 1).reshape(E, 4, n, n)
+
+
+@pytest.mark.parametrize("n", [4, 5, 7, 8, 10, 16])
+def test_observation_kernels_every_layout_and_alignment(torch_cuda, n):
+    """Vector-store quad kernel (N*N % 4 == 0, aligned out) and the scalar kernel
+    (odd N, or an out pointer off the 4-element alignment) write the same values
+    as a numpy restatement, for every layout and dtype, on mid-game boards."""
+    torch = torch_cuda
+    E = 1000
+    env = make_env(torch, E, n, auto=True, seed=5)
+    env.step_policy("random", n_plies=n * n // 2 + 3, record=False)
+    b, m, lg = get_state_np(env)
+    for layout in ("board", "board_legal", "make_state", "absolute"):
+        want = _obs_np(n, b, m, lg, layout)
+        for dt in (torch.int8, torch.int32, torch.int64, torch.float32, torch.float64):
+            got = env.observe(layout, dt)
+            np.testing.assert_array_equal(got.cpu().numpy(), want, err_msg="%s %s" % (layout, dt))
+            buf = torch.empty(want.size + 1, dtype=dt, device=got.device)
+            off = buf[1:].view(want.shape)  # base one element past the vector alignment
+            env.observe(layout, dt, out=off)
+            np.testing.assert_array_equal(off.cpu().numpy(), want, err_msg="unaligned %s %s" % (layout, dt))
