@@ -65,6 +65,15 @@ OTH_HD BB<W>& operator&=(BB<W>& a, const BB<W>& b) {
     a = a & b;
     return a;
 }
+// c ? a : b word by word (a select of two structs' addresses can force them into scratch)
+template <int W>
+OTH_HD BB<W> pick(bool c, const BB<W>& a, const BB<W>& b) {
+    BB<W> r;
+#pragma unroll
+    for (int i = 0; i < W; ++i) r.w[i] = c ? a.w[i] : b.w[i];
+    return r;
+}
+
 template <int W>
 OTH_HD bool any(const BB<W>& a) {
     uint64_t x = 0;
@@ -109,6 +118,13 @@ OTH_HD int popc64(uint64_t x) {
     return __popcll(x);
 #else
     return __builtin_popcountll(x);
+#endif
+}
+OTH_HD int clz64(uint64_t x) {  // x != 0
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __clzll(x);
+#else
+    return __builtin_clzll(x);
 #endif
 }
 template <int W>
@@ -388,7 +404,8 @@ OTH_HD void legal_dir(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O, BB<Geo<N>:
 // per-shift edge masks are needed.  The -S doubling chain is the +S chain
 // shifted: p2-(y) = p2+(y+S), p4-(y) = p4+(y+3S), p8-(y) = p8+(y+7S).
 template <int N, int S>
-OTH_HD void legal_axis(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& p1, BB<Geo<N>::W>& L) {
+OTH_HD void legal_axis(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& p1, BB<Geo<N>::W>& L, BB<Geo<N>::W>& tplus,
+                       BB<Geo<N>::W>& tminus) {
     constexpr int W = Geo<N>::W;
     constexpr int STEPS = Pro<N, 0, 1>::STEPS;
     // The last doubling step may reuse the previous propagator when that still
@@ -412,6 +429,7 @@ OTH_HD void legal_axis(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& p1, BB<Geo<N
             if constexpr (R4) t |= p4 & shift<W, 4 * S>(t);
             else t |= p8 & shift<W, 8 * S>(t);
         }
+        tplus = t;
         L |= shift<W, S>(t);
     }
     {  // -S
@@ -434,8 +452,14 @@ OTH_HD void legal_axis(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& p1, BB<Geo<N
             if constexpr (R4) t |= p4m & shift<W, -4 * S>(t);
             else t |= shift<W, -7 * S>(p8) & shift<W, -8 * S>(t);
         }
+        tminus = t;
         L |= shift<W, -S>(t);
     }
+}
+template <int N, int S>
+OTH_HD void legal_axis(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& p1, BB<Geo<N>::W>& L) {
+    BB<Geo<N>::W> tp, tm;  // fills not kept
+    legal_axis<N, S>(P, p1, L, tp, tm);
 }
 
 // get_possible_actions (othello.py:313-343) as a mask: empty squares from
@@ -462,6 +486,81 @@ OTH_HD BB<Geo<N>::W> legal_moves(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O)
     legal_dir<N, -1, -1>(P, O, L);
 #endif
     return L & ~(P | O) & Geo<N>::BOARD;
+}
+
+// legal_moves that keeps the eight fills (any W): t[d] = the opponent discs
+// from which an own disc is reached going along ray direction d through
+// opponent discs only (d = 0..3: E, S, SE, SW toward higher squares; 4..7: W,
+// N, NW, NE).  The scan stepping +S from the own discs yields the fill of
+// direction -S and vice versa.
+template <int N>
+OTH_HD BB<Geo<N>::W> legal_moves_fills(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O, BB<Geo<N>::W> t[8]) {
+    auto L = zero<Geo<N>::W>();
+    const auto pin = O & Geo<N>::INNER;
+    legal_axis<N, 1>(P, pin, L, t[4], t[0]);      // W / E
+    legal_axis<N, N>(P, O, L, t[5], t[1]);        // N / S
+    legal_axis<N, N + 1>(P, pin, L, t[6], t[2]);  // NW / SE
+    legal_axis<N, N - 1>(P, pin, L, t[7], t[3]);  // NE / SW
+    return L & ~(P | O) & Geo<N>::BOARD;
+}
+
+// update_board's flips (othello.py:391-410) from the fills of the side to
+// move and the ray table rays[d * N*N + a] (the squares strictly beyond a in
+// direction d): along ray d the run to flip is the part of the ray before its
+// first square outside t[d] (every fill square on that run is capped further
+// along d).  Toward higher squares that square is the lowest set bit of
+// ray & ~t[d] over the words in ascending order, toward lower squares the
+// highest over the words in descending order.  The last square of a ray is
+// never in a fill, so a non-empty ray always has one.
+template <int N>
+OTH_HD BB<Geo<N>::W> flips_fills(const BB<Geo<N>::W>* rays, const BB<Geo<N>::W> t[8], int a) {
+    constexpr int W = Geo<N>::W;
+    constexpr int NN = N * N;
+    auto f = zero<W>();
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const BB<W> ray = rays[d * NN + a];
+        bool found = false;
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+            const uint64_t y = ray.w[i] & ~t[d].w[i];
+            const uint64_t fi = ray.w[i] & ((y & (0ull - y)) - 1ull);  // y == 0: the whole word
+            f.w[i] |= found ? 0ull : fi;
+            found = found || y != 0ull;
+        }
+    }
+#pragma unroll
+    for (int d = 4; d < 8; ++d) {
+        const BB<W> ray = rays[d * NN + a];
+        bool found = false;
+#pragma unroll
+        for (int i = W - 1; i >= 0; --i) {
+            const uint64_t y = ray.w[i] & ~t[d].w[i];
+            const uint64_t hb = 0x8000000000000000ull >> clz64(y | 1ull);
+            const uint64_t fi = y ? (ray.w[i] & (0ull - (hb << 1))) : ray.w[i];
+            f.w[i] |= found ? 0ull : fi;
+            found = found || y != 0ull;
+        }
+    }
+    return f;
+}
+
+// ray table of fills_flips: rays[d * N*N + sq] for the eight directions
+template <int N>
+OTH_HD BB<Geo<N>::W> ray_from(int d, int sq) {
+    // d: E, S, SE, SW, W, N, NW, NE (no tables: a runtime-indexed local array would live in scratch)
+    const int dr = d == 0 || d == 4 ? 0 : (d < 4 ? 1 : -1);
+    const int dc = d == 1 || d == 5 ? 0 : (d == 0 || d == 2 || d == 7 ? 1 : -1);
+    auto r = zero<Geo<N>::W>();
+    int row = sq / N + dr, col = sq % N + dc;
+    while (row >= 0 && row < N && col >= 0 && col < N) {
+        const int b = row * N + col;
+#pragma unroll
+        for (int i = 0; i < Geo<N>::W; ++i) r.w[i] |= (b / 64 == i) ? 1ull << (b % 64) : 0ull;  // no dynamic word index
+        row += dr;
+        col += dc;
+    }
+    return r;
 }
 
 template <int N, int DR, int DC>

@@ -53,6 +53,12 @@ using namespace oth;
 #ifndef OTH_GREEDY_PLANES
 #define OTH_GREEDY_PLANES 1  // GreedyPolicy on bit planes for N <= 8 (bitboard.hpp OneWord::greedy)
 #endif
+#ifndef OTH_FILLS_W
+#define OTH_FILLS_W 1  // FillsW engine (ray tables + fills) for multi-word boards
+#endif
+#ifndef OTH_FILLS_W_MAXN
+#define OTH_FILLS_W_MAXN 16  // its BB<W> ray table: 8 * N*N * W words of LDS (16x16: 64 KiB; +30 % at 16x16 all the same)
+#endif
 #ifndef OTH_PICKED
 #define OTH_PICKED 1  // k_play: the action is a pick from the legal mask, flips without a validity branch
 #endif
@@ -326,10 +332,51 @@ struct Fills {
     // recompute the fills for the side to move (after a load or a reset)
     __device__ __forceinline__ void prime(const Lane<N>& s) const {
         const bool tw = (s.meta & M_TURN_WHITE) != 0;
-        (void)legal(tw ? s.white : s.black, tw ? s.black : s.white);
+        (void)legal(pick(tw, s.white, s.black), pick(tw, s.black, s.white));
     }
     __device__ __forceinline__ bool leader() const { return true; }
 };
+
+// FillsW<N>: the Fills engine for multi-word boards (N >= 9): the legal scan
+// keeps its eight fills (legal_moves_fills) and update_board's flips come from
+// them and a ray table of BB<W> entries in LDS (flips_fills), without the
+// Kogge-Stone run and capping test per direction.
+template <int N>
+struct FillsW {
+    static constexpr int W = Geo<N>::W;
+    static constexpr int LANES = 1;
+    static constexpr int RAY_WORDS = 8 * N * N * W;
+    const BB<W>* rays;
+    mutable BB<W> t[8];
+    __device__ __forceinline__ FillsW(int, const uint64_t* lds) : rays(reinterpret_cast<const BB<W>*>(lds)) {}
+    __device__ __forceinline__ BB<W> legal(const BB<W>& P, const BB<W>& O) const {
+        return legal_moves_fills<N>(P, O, t);
+    }
+    __device__ __forceinline__ BB<W> flip(const BB<W>&, const BB<W>&, int a) const {
+        return flips_fills<N>(rays, t, a);
+    }
+    __device__ __forceinline__ void prime(const Lane<N>& s) const {
+        const bool tw = (s.meta & M_TURN_WHITE) != 0;
+        BB<W> P, O;  // word-wise selects: a select of the two members' addresses puts the lane in scratch
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+            P.w[i] = tw ? s.white.w[i] : s.black.w[i];
+            O.w[i] = tw ? s.black.w[i] : s.white.w[i];
+        }
+        (void)legal(P, O);
+    }
+    __device__ __forceinline__ bool leader() const { return true; }
+    __device__ static void fill(uint64_t* lds) {
+        BB<W>* r = reinterpret_cast<BB<W>*>(lds);
+        for (int i = threadIdx.x; i < 8 * N * N; i += BLOCK) r[i] = ray_from<N>(i / (N * N), i % (N * N));
+        __syncthreads();
+    }
+};
+
+template <typename Eng>
+struct is_fills_w : std::false_type {};
+template <int N>
+struct is_fills_w<FillsW<N>> : std::true_type {};
 
 // the other lane of the pair (lanes 2k, 2k+1): DPP quad_perm [1,0,3,2]
 __device__ __forceinline__ uint32_t pair_swap32(uint32_t x) {
@@ -460,13 +507,8 @@ __device__ __forceinline__ void finish_step(Lane<N>& s, bool tw, bool valid, con
             winner = by_count;
         }
     }
-    if (tw) {
-        s.white = P;
-        s.black = O;
-    } else {
-        s.black = P;
-        s.white = O;
-    }
+    s.white = pick(tw, P, O);  // word-wise: a store through a selected member address puts the lane in scratch
+    s.black = pick(tw, O, P);
     int r = 0;  // :444-461
     if (term) {
         if (flags & OTH_DISK_REWARD) {
@@ -498,10 +540,9 @@ __device__ __forceinline__ void step_lane(Lane<N>& s, int a, uint32_t flags, int
         return;
     }
     const bool tw = (s.meta & M_TURN_WHITE) != 0;
-    BB<W> P = tw ? s.white : s.black;
-    BB<W> O = tw ? s.black : s.white;
-    if constexpr (PICKED && Eng::RAY_WORDS > 0) {
-        static_assert(W == 1, "ray engines are one-word");
+    BB<W> P = pick(tw, s.white, s.black);
+    BB<W> O = pick(tw, s.black, s.white);
+    if constexpr (PICKED && Eng::RAY_WORDS > 0 && W == 1) {
         const bool valid = a >= 0;
         const uint64_t m = valid ? 1ull << (a & 63) : 0ull;
 #ifdef OTH_ABLATE_NOFLIP  // timing ablation only
@@ -544,8 +585,8 @@ __device__ __forceinline__ void greedy_scan(const Lane<N>& s, int parity, int st
                                             const Eng& eng) {
     constexpr int W = Geo<N>::W;
     const bool tw = (s.meta & M_TURN_WHITE) != 0;
-    const BB<W> P = tw ? s.white : s.black;
-    const BB<W> O = tw ? s.black : s.white;
+    const BB<W> P = pick(tw, s.white, s.black);
+    const BB<W> O = pick(tw, s.black, s.white);
     best = -1;
     best_cnt = -1;
     int idx = 0;  // rank of the candidate among the legal moves
@@ -642,7 +683,7 @@ template <int N, int D>
 __device__ __forceinline__ int maximin_action(const Lane<N>& s) {
     const bool tw = (s.meta & M_TURN_WHITE) != 0;
     int move;
-    maximin_node<N, D, 0>(tw ? s.white : s.black, tw ? s.black : s.white, s.legal, move);
+    maximin_node<N, D, 0>(pick(tw, s.white, s.black), pick(tw, s.black, s.white), s.legal, move);
     return move;
 }
 
@@ -769,8 +810,9 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
                                                 int32_t* __restrict__ actions, int32_t* __restrict__ rewards,
                                                 uint8_t* __restrict__ dones, unsigned long long* __restrict__ wdl,
                                                 Rng rng, uint64_t ply0) {
-    __shared__ uint64_t lds_rays[Eng::RAY_WORDS > 0 ? Eng::RAY_WORDS : 1];
-    if constexpr (Eng::RAY_WORDS > 0) fill_rays<N>(lds_rays);
+    __shared__ __attribute__((aligned(16))) uint64_t lds_rays[Eng::RAY_WORDS > 0 ? Eng::RAY_WORDS : 1];
+    if constexpr (is_fills_w<Eng>::value) Eng::fill(lds_rays);
+    else if constexpr (Eng::RAY_WORDS > 0) fill_rays<N>(lds_rays);
     const int gt = blockIdx.x * BLOCK + threadIdx.x;
     const int e = gt / Eng::LANES;
     const Eng eng(gt % Eng::LANES, lds_rays);

@@ -77,6 +77,9 @@ int launch_play(oth_env* env, int policy, int n_plies, int32_t* actions, int32_t
         } else if constexpr (Geo<N>::W == 1 && OTH_FILLS &&
                              (POL == OTH_POLICY_RANDOM || (OTH_FILLS_GREEDY && POL == OTH_POLICY_GREEDY))) {
             launch_k_play<N, POL, Fills<N>>(1, env, n_plies, actions, rewards, dones, ply0, st);
+        } else if constexpr (Geo<N>::W > 1 && OTH_FILLS_W && N <= OTH_FILLS_W_MAXN &&
+                             (POL == OTH_POLICY_RANDOM || POL == OTH_POLICY_GREEDY)) {
+            launch_k_play<N, POL, FillsW<N>>(1, env, n_plies, actions, rewards, dones, ply0, st);
         } else if constexpr (Geo<N>::W == 1 && OTH_RAYS && POL == OTH_POLICY_RANDOM) {
             // random play with OTH_FILLS=0: ray-table flips with the capping test
             // (greedy keeps Kogge-Stone flips there: the ray tables' exposed LDS

@@ -51,6 +51,31 @@ static void greedy_planes_n(int E, const uint64_t* mover, const uint64_t* opp, c
     }
 }
 
+// legal_moves_fills + flips_fills (the multi-word fills engine) from every
+// square a with legal[a] set: out[e * W * NN + a * W ..] = the flips (0 elsewhere)
+template <int N>
+static void fills_flips_n(int E, const uint64_t* mover, const uint64_t* opp, uint64_t* legal, uint64_t* out) {
+    constexpr int W = Geo<N>::W;
+    constexpr int NN = N * N;
+    static BB<W> rays[8 * NN];
+    for (int d = 0; d < 8; ++d)
+        for (int a = 0; a < NN; ++a) rays[d * NN + a] = ray_from<N>(d, a);
+    for (int e = 0; e < E; ++e) {
+        BB<W> P, O, t[8];
+        for (int i = 0; i < W; ++i) {
+            P.w[i] = mover[e * W + i];
+            O.w[i] = opp[e * W + i];
+        }
+        const BB<W> L = legal_moves_fills<N>(P, O, t);
+        memcpy(legal + e * W, L.w, sizeof(L.w));
+        for (int a = 0; a < NN; ++a) {
+            BB<W> f = zero<W>();
+            if ((L.w[a / 64] >> (a % 64)) & 1u) f = flips_fills<N>(rays, t, a);
+            memcpy(out + ((size_t)e * NN + a) * W, f.w, sizeof(f.w));
+        }
+    }
+}
+
 #define DISPATCH8(fn, ...)                 \
     switch (n) {                           \
         case 4: fn<4>(__VA_ARGS__); break; \
@@ -86,6 +111,10 @@ int host_legal(int n, int E, const uint64_t* mover, const uint64_t* opp, uint64_
 }
 int host_flips(int n, int E, const uint64_t* mover, const uint64_t* opp, const int32_t* sq, uint64_t* out) {
     DISPATCH(flips_n, E, mover, opp, sq, out);
+    return 0;
+}
+int host_fills_flips(int n, int E, const uint64_t* mover, const uint64_t* opp, uint64_t* legal, uint64_t* out) {
+    DISPATCH(fills_flips_n, E, mover, opp, legal, out);
     return 0;
 }
 int host_legal_fills(int n, int E, const uint64_t* mover, const uint64_t* opp, uint64_t* out, uint64_t* fills) {

@@ -31,6 +31,7 @@ def hostlib():
     L.host_select.argtypes = [ctypes.c_uint64, ctypes.c_int]
     L.host_legal_fills.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P]
     L.host_greedy_planes.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P]
+    L.host_fills_flips.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P]
     L.host_philox4.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32, P]
     return L
 
@@ -167,3 +168,30 @@ def test_select_and_philox(hostlib):
     out = np.zeros(4, dtype=np.uint32)
     hostlib.host_philox4(0, 0, 0, 0, ptr(out))
     assert [hex(v) for v in out] == ["0x6627e8d5", "0xe169c58d", "0xbc57ac4c", "0x9b00dbd8"]
+
+
+@pytest.mark.parametrize("n", [4, 6, 8, 9, 10, 11, 12, 14, 16])
+def test_multiword_fills_engine_host_build(hostlib, n):
+    """legal_moves_fills == legal_moves (the oracle's legal moves) and, from
+    every legal square, flips_fills (ray tables + the scan's fills, no capping
+    test) == flips<N> (Kogge-Stone runs with the capping test) -- the FillsW
+    engine's two halves, for one- and multi-word boards."""
+    rng = np.random.RandomState(300 + n)
+    W = oracle.nwords(n)
+    for density in (0.3, 0.6, 0.9):
+        E = 300
+        _, mover, opp = random_boards(n, E, rng, density)
+        legal = np.zeros_like(mover)
+        out = np.zeros((E, n * n, W), dtype=np.uint64)
+        assert hostlib.host_fills_flips(n, E, ptr(mover), ptr(opp), ptr(legal), ptr(out)) == 0
+        np.testing.assert_array_equal(legal, oracle.legal(n, mover, opp))
+        es, sqs = [], []
+        for e in range(E):
+            for a in range(n * n):
+                if (int(legal[e, a // 64]) >> (a % 64)) & 1:
+                    es.append(e)
+                    sqs.append(a)
+        want = np.zeros((len(es), W), dtype=np.uint64)
+        assert hostlib.host_flips(n, len(es), ptr(mover[es].copy()), ptr(opp[es].copy()),
+                                  ptr(np.array(sqs, dtype=np.int32)), ptr(want)) == 0
+        np.testing.assert_array_equal(out[es, sqs], want)

@@ -138,7 +138,12 @@ def test_random_rollout_replays_on_oracle(torch_cuda, n, E, plies):
                          [(4, "random", True, True, True, 0), (5, "random", False, True, True, 4),
                           (7, "random", True, False, False, 0), (8, "random", False, False, True, 6),
                           (4, "greedy", True, True, True, 2), (7, "greedy", False, False, True, 6),
-                          (5, "greedy", True, False, False, 4)])
+                          (5, "greedy", True, False, False, 4),
+                          # multi-word boards: the FillsW engine (BB<W> ray tables + fills)
+                          (9, "random", False, True, True, 4), (10, "greedy", True, False, True, 6),
+                          (11, "random", True, True, False, 0), (12, "greedy", False, False, True, 4),
+                          (14, "random", True, False, True, 2), (16, "random", False, True, True, 0),
+                          (16, "greedy", True, False, True, 4)])
 def test_fills_engine_flag_combinations(torch_cuda, n, policy, sd, dr, auto, init_rand):
     """The fills engine (flips from the legal scan carried across plies) under
     every flag combination, with and without auto-reset and random openings:
@@ -173,7 +178,7 @@ def test_rollout_split_over_launches_is_identical(torch_cuda):
         assert torch.equal(x, y)
 
 
-@pytest.mark.parametrize("n,init_rand", [(8, 10), (6, 4)])
+@pytest.mark.parametrize("n,init_rand", [(8, 10), (6, 4), (10, 6)])
 def test_greedy_rollout_replays_on_oracle(torch_cuda, n, init_rand):
     """Config 3: greedy vs greedy after Philox random openings (0..init_rand plies)."""
     torch = torch_cuda
