@@ -276,6 +276,28 @@ OTH_HD uint64_t to64(V v) {
 #ifndef OTH_GREEDY_WORD64
 #define OTH_GREEDY_WORD64 1  // OneWord::greedy on uint64_t (1); dword pairs (0) miscompile inside k_play on gfx950, see DESIGN.md
 #endif
+#ifndef OTH_GREEDY_BITOP3
+#define OTH_GREEDY_BITOP3 1  // greedy plane adders as explicit 3-input v_bitop3_b32 (xor3 / majority) per dword
+#endif
+// a ^ b ^ c and majority(a, b, c): symmetric, so the builtin's operand order does not matter
+OTH_HD uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, 0x96);
+    const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), 0x96);
+    return ((uint64_t)hi << 32) | lo;
+#else
+    return a ^ b ^ c;
+#endif
+}
+OTH_HD uint64_t maj3_64(uint64_t a, uint64_t b, uint64_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, 0xE8);
+    const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), 0xE8);
+    return ((uint64_t)hi << 32) | lo;
+#else
+    return (a & b) | (c & (a | b));
+#endif
+}
 #ifndef OTH_GREEDY_MASKSEL
 #define OTH_GREEDY_MASKSEL 0  // OneWord::greedy's plane narrowing with mask arithmetic instead of a select
 #endif
@@ -656,7 +678,10 @@ struct OneWord {
         if constexpr (R >= 4) A4 = A2 & sh<-2 * S>(A2);
         if constexpr (R >= 5) A5 = A4 & sh<-4 * S>(A1);
         if constexpr (R >= 6) A6 = A4 & sh<-4 * S>(A2);
-        out[0] = A1 ^ A2 ^ A3 ^ A4 ^ A5 ^ A6;
+        if constexpr (std::is_same<V, uint64_t>::value && OTH_GREEDY_BITOP3)
+            out[0] = xor3_64(xor3_64(A1, A2, A3), A4, A5) ^ A6;
+        else
+            out[0] = A1 ^ A2 ^ A3 ^ A4 ^ A5 ^ A6;
         out[1] = (A2 ^ A4) | A6;
         out[2] = A4;
     }
@@ -668,8 +693,18 @@ struct OneWord {
 #pragma unroll
         for (int i = 0; i < NO; ++i) {
             const V x = i < NA ? a[i] : z, y = i < NB ? b[i] : z;
-            out[i] = x ^ y ^ c;
-            c = (x & y) | (c & (x | y));
+            if constexpr (std::is_same<V, uint64_t>::value && OTH_GREEDY_BITOP3) {
+                if (i == 0) {  // half adder: no carry in
+                    out[i] = x ^ y;
+                    c = x & y;
+                } else {  // full adder: one 3-input op per dword for the sum and one for the carry
+                    out[i] = xor3_64(x, y, c);
+                    c = maj3_64(x, y, c);
+                }
+            } else {
+                out[i] = x ^ y ^ c;
+                c = (x & y) | (c & (x | y));
+            }
         }
     }
     // GreedyPolicy.get_action (simple_policies.py:69-92): the candidate (a

@@ -113,7 +113,8 @@ def test_games_in_lockstep(torch_cuda, golden_dir, n):
                     assert dn[gi] == 1 and rew[gi] == 0
 
 
-@pytest.mark.parametrize("n,E,plies", [(8, 65536, 130), (6, 16384, 80), (10, 8192, 200), (16, 1024, 260)])
+@pytest.mark.parametrize("n,E,plies", [(8, 65536, 130), (6, 16384, 80), (10, 8192, 200), (16, 1024, 260),
+                                        (8, 1, 150), (8, 777, 100), (12, 333, 180)])
 def test_random_rollout_replays_on_oracle(torch_cuda, n, E, plies):
     """Config 2 / 5: on-device random play with auto-reset; every action, reward,
     done, the final state and the W/D/L tally equal the oracle's replay."""
@@ -131,7 +132,7 @@ def test_random_rollout_replays_on_oracle(torch_cuda, n, E, plies):
     np.testing.assert_array_equal(m, s.meta)
     np.testing.assert_array_equal(lg, s.legal)
     np.testing.assert_array_equal(wdl, owdl)
-    assert owdl.sum() >= E  # at least one finished game per board
+    assert owdl.sum() >= E  # at least one finished game per board (ragged E: blocks past E store nothing)
 
 
 @pytest.mark.parametrize("n,policy,sd,dr,auto,init_rand",
