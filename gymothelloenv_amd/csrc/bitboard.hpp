@@ -289,6 +289,15 @@ OTH_HD uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) {
     return a ^ b ^ c;
 #endif
 }
+OTH_HD uint64_t and3_64(uint64_t a, uint64_t b, uint64_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, 0x80);
+    const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), 0x80);
+    return ((uint64_t)hi << 32) | lo;
+#else
+    return a & b & c;
+#endif
+}
 OTH_HD uint64_t maj3_64(uint64_t a, uint64_t b, uint64_t c) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, 0xE8);

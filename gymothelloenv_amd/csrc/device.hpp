@@ -62,6 +62,12 @@ using namespace oth;
 #ifndef OTH_PICKED
 #define OTH_PICKED 1  // k_play: the action is a pick from the legal mask, flips without a validity branch
 #endif
+#ifndef OTH_FLIP_AND3
+#define OTH_FLIP_AND3 1  // Fills::flip toward higher squares as one 3-input AND (v_bitop3_b32) per dword
+#endif
+#ifndef OTH_DRAW_UNROLL
+#define OTH_DRAW_UNROLL 1  // k_play random: four plies unrolled per Philox block (no per-ply word rotation)
+#endif
 #ifndef OTH_DRAW_ROTATE
 #define OTH_DRAW_ROTATE 1  // k_play random: rotate the 4-word Philox block per ply instead of picking word g % 4
 #endif
@@ -313,7 +319,12 @@ struct Fills {
         for (int d = 0; d < 4; ++d) {  // toward higher squares: cap = lowest ray square outside the fill
             const uint64_t ray = r[64 * d];
             const uint64_t y = ray & ~t[d];
+#if OTH_FLIP_AND3
+            // ray & ((y & -y) - 1) == ray & t & (y - 1): one 3-input AND per dword
+            f |= and3_64(ray, t[d], y - 1ull);
+#else
             f |= ray & ((y & (0ull - y)) - 1ull);
+#endif
         }
 #pragma unroll
         for (int d = 4; d < 8; ++d) {  // toward lower squares: cap = highest ray square outside the fill
@@ -823,35 +834,18 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
         Lane<N> s;
         load_lane<N>(s, boards, meta, legal, e);
         eng.prime(s);
-        U4 draws{0, 0, 0, 0};
         int32_t* act_p = actions + e;
         int32_t* rew_p = rewards + e;
         uint8_t* done_p = dones + e;
-        for (int p = 0; p < plies; ++p) {
+        // one ply; u_rand = the random policy's 32-bit draw for this ply
+        auto ply = [&](int p, uint32_t u_rand) __attribute__((always_inline)) {
             const uint64_t g = ply0 + (uint64_t)p;
             const size_t o = (size_t)p * (size_t)E + (size_t)e;
-            // random policy: one Philox block per 4 plies (g uniform: no divergence)
-#ifdef OTH_ABLATE_RNG  // timing ablation only: a multiplicative hash instead of Philox
-            if (POLICY == OTH_POLICY_RANDOM && (p == 0 || (g & 3) == 0)) {
-                const uint32_t h = (id ^ (uint32_t)g) * 0x9E3779B9u;
-                draws = U4{h, h * 3u, h * 5u, h * 7u};
-            }
-#else
-            if (POLICY == OTH_POLICY_RANDOM && (p == 0 || (g & 3) == 0)) {
-                draws = philox4(rng.seed, id, g >> 2, RNG_ACTION);
-#if OTH_DRAW_ROTATE
-                // draws.x is always this ply's word: rotate to word g % 4 at the launch's first ply
-                if (p == 0)
-                    for (uint32_t j = 0; j < (uint32_t)(g & 3); ++j) draws = U4{draws.y, draws.z, draws.w, draws.x};
-#endif
-            }
-#endif
             int a = -1, r = 0, d = 1, win = NO_DISK;
             if (!(s.meta & M_TERMINATED)) {
                 const uint32_t rl = s.meta >> M_RAND_SHIFT;
                 if (POLICY == OTH_POLICY_RANDOM || rl > 0) {
-                    const uint32_t u = POLICY == OTH_POLICY_RANDOM ? (OTH_DRAW_ROTATE ? draws.x : pick4(draws, (uint32_t)(g & 3)))
-                                                                   : action_draw(rng.seed, id, g);
+                    const uint32_t u = POLICY == OTH_POLICY_RANDOM ? u_rand : action_draw(rng.seed, id, g);
 #ifdef OTH_ABLATE_SELECT  // timing ablation only: lowest legal square
                     a = __builtin_ctzll(s.legal.w[0] | (1ull << 63)) + (int)(u & 0);
 #else
@@ -872,7 +866,6 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
                     }
                 }
             }
-            if (POLICY == OTH_POLICY_RANDOM && OTH_DRAW_ROTATE) draws = U4{draws.y, draws.z, draws.w, draws.x};
 #ifndef OTH_ABLATE_NOSTORE
             if (lead) {
                 if constexpr (REC) {  // running pointers: one 64-bit add each per ply
@@ -889,6 +882,52 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
                 }
             }
 #endif
+        };
+#if OTH_DRAW_UNROLL && !defined(OTH_ABLATE_RNG)
+        if constexpr (POLICY == OTH_POLICY_RANDOM) {
+            // Philox block g/4 gives plies 4k..4k+3 their words x, y, z, w: four
+            // plies unrolled per block once g is 4-aligned (g is uniform, so
+            // these branches are scalar); single plies before and after
+            int p = 0;
+            while (p < plies) {
+                const uint64_t g = ply0 + (uint64_t)p;
+                const U4 d4 = philox4(rng.seed, id, g >> 2, RNG_ACTION);
+                if ((g & 3) == 0 && p + 4 <= plies) {
+                    ply(p, d4.x);
+                    ply(p + 1, d4.y);
+                    ply(p + 2, d4.z);
+                    ply(p + 3, d4.w);
+                    p += 4;
+                } else {
+                    ply(p, pick4(d4, (uint32_t)(g & 3)));
+                    ++p;
+                }
+            }
+        } else
+#endif
+        {
+            U4 draws{0, 0, 0, 0};
+            for (int p = 0; p < plies; ++p) {
+                const uint64_t g = ply0 + (uint64_t)p;
+                // random policy: one Philox block per 4 plies (g uniform: no divergence)
+#ifdef OTH_ABLATE_RNG  // timing ablation only: a multiplicative hash instead of Philox
+                if (POLICY == OTH_POLICY_RANDOM && (p == 0 || (g & 3) == 0)) {
+                    const uint32_t h = (id ^ (uint32_t)g) * 0x9E3779B9u;
+                    draws = U4{h, h * 3u, h * 5u, h * 7u};
+                }
+#else
+                if (POLICY == OTH_POLICY_RANDOM && (p == 0 || (g & 3) == 0)) {
+                    draws = philox4(rng.seed, id, g >> 2, RNG_ACTION);
+#if OTH_DRAW_ROTATE
+                    // draws.x is always this ply's word: rotate to word g % 4 at the launch's first ply
+                    if (p == 0)
+                        for (uint32_t j = 0; j < (uint32_t)(g & 3); ++j) draws = U4{draws.y, draws.z, draws.w, draws.x};
+#endif
+                }
+#endif
+                ply(p, OTH_DRAW_ROTATE ? draws.x : pick4(draws, (uint32_t)(g & 3)));
+                if (POLICY == OTH_POLICY_RANDOM && OTH_DRAW_ROTATE) draws = U4{draws.y, draws.z, draws.w, draws.x};
+            }
         }
         if (lead) store_lane<N>(s, boards, meta, legal, e);
     }
