@@ -120,6 +120,9 @@ OTH_HD int popc64(uint64_t x) {
     return __builtin_popcountll(x);
 #endif
 }
+OTH_HD int ctz64(uint64_t x) {  // x != 0
+    return __builtin_ctzll(x);
+}
 OTH_HD int clz64(uint64_t x) {  // x != 0
 #if defined(__HIP_DEVICE_COMPILE__)
     return __clzll(x);
@@ -575,6 +578,93 @@ OTH_HD BB<Geo<N>::W> flips_fills(const BB<Geo<N>::W>* rays, const BB<Geo<N>::W> 
     }
     return f;
 }
+
+// GreedyPolicy on bit planes for any W (OneWord::greedy's algorithm on BB<W>):
+// per direction the run length of every square from the fills as K-bit
+// planes, the eight summed, the argmax narrowed plane by plane from the top.
+template <int N>
+struct PlanesW {
+    static constexpr int W = Geo<N>::W;
+    static constexpr int R = N - 2;  // longest run
+    static constexpr int bits(int v) { return v < 2 ? 1 : 1 + bits(v / 2); }
+    static constexpr int K = bits(R);      // planes of one run length
+    static constexpr int T = bits(8 * R);  // planes of the sum over the 8 directions
+    static constexpr int hi_of(int j) { return j >= 8 ? 8 : (j >= 4 ? 4 : (j >= 2 ? 2 : 1)); }
+
+    // A[j] = {a : a + S, ..., a + jS all in the fill} (nested): A[1] = the fill
+    // stepped back once; A[j] = A[hi] & (A[j - hi] stepped back hi times), hi the
+    // largest power of two below j (A[2h] = A[h] & A[h] stepped back h).  Off-board
+    // squares a shift reaches never come back: every shift of one direction goes
+    // the same way.
+    template <int S, int J>
+    static OTH_HD void fill_A(BB<W>* A) {
+        if constexpr (J <= R) {
+            constexpr int H = hi_of(J);
+            if constexpr (H == J) A[J] = A[H / 2] & shift<W, -(H / 2) * S>(A[H / 2]);
+            else A[J] = A[H] & shift<W, -H * S>(A[J - H]);
+            fill_A<S, J + 1>(A);
+        }
+    }
+    // run length of every square along step S as K bit planes: bit k = XOR of
+    // the A[j] with j a multiple of 2^k
+    template <int S>
+    static OTH_HD void run_len(const BB<W>& fill, BB<W>* out) {
+        BB<W> A[R + 1];
+        A[0] = zero<W>();
+        A[1] = shift<W, -S>(fill);
+        fill_A<S, 2>(A);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            BB<W> b = zero<W>();
+#pragma unroll
+            for (int j = 1 << k; j <= R; j += 1 << k) b = b ^ A[j];
+            out[k] = b;
+        }
+    }
+    // out[0..NO) = a[0..NA) + b[0..NB) (ripple carry, carries past NO dropped)
+    template <int NA, int NB, int NO>
+    static OTH_HD void add(const BB<W>* a, const BB<W>* b, BB<W>* out) {
+        BB<W> c = zero<W>();
+#pragma unroll
+        for (int i = 0; i < NO; ++i) {
+            const BB<W> x = i < NA ? a[i] : zero<W>(), y = i < NB ? b[i] : zero<W>();
+            out[i] = x ^ y ^ c;
+            c = (x & y) | (c & (x | y));
+        }
+    }
+    static constexpr int min_(int a, int b) { return a < b ? a : b; }
+    // GreedyPolicy.get_action (simple_policies.py:69-92): the candidate of
+    // `legal` flipping the most discs, the lowest of equal counts; -1 without one
+    static OTH_HD int greedy(const BB<W> t[8], const BB<W>& legal) {
+        constexpr int K1 = min_(K + 1, T), K2 = min_(K + 2, T);
+        BB<W> n[8][K];
+        run_len<1>(t[0], n[0]);
+        run_len<N>(t[1], n[1]);
+        run_len<N + 1>(t[2], n[2]);
+        run_len<N - 1>(t[3], n[3]);
+        run_len<-1>(t[4], n[4]);
+        run_len<-N>(t[5], n[5]);
+        run_len<-N - 1>(t[6], n[6]);
+        run_len<-N + 1>(t[7], n[7]);
+        BB<W> s1[4][K1], s2[2][K2], tot[T];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) add<K, K, K1>(n[2 * i], n[2 * i + 1], s1[i]);
+        add<K1, K1, K2>(s1[0], s1[1], s2[0]);
+        add<K1, K1, K2>(s1[2], s1[3], s2[1]);
+        add<K2, K2, T>(s2[0], s2[1], tot);
+        BB<W> cand = legal;
+#pragma unroll
+        for (int i = T - 1; i >= 0; --i) {
+            const BB<W> h = cand & tot[i];
+            cand = pick(any(h), h, cand);
+        }
+        int res = -1;
+#pragma unroll
+        for (int i = W - 1; i >= 0; --i)
+            if (cand.w[i]) res = 64 * i + ctz64(cand.w[i]);
+        return res;
+    }
+};
 
 // ray table of fills_flips: rays[d * N*N + sq] for the eight directions
 template <int N>

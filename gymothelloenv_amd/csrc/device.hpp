@@ -50,6 +50,12 @@ using namespace oth;
 #ifndef OTH_U32
 #define OTH_U32 1  // Fills engine scans on dword pairs (bitboard.hpp U2)
 #endif
+#ifndef OTH_SOLO_U32
+#define OTH_SOLO_U32 1  // Solo engine (k_step, k_step_vs, ...) scans on dword pairs too for N <= 8
+#endif
+#ifndef OTH_GREEDY_PLANES_W
+#define OTH_GREEDY_PLANES_W 1  // GreedyPolicy on bit planes for multi-word boards too (bitboard.hpp PlanesW)
+#endif
 #ifndef OTH_GREEDY_PLANES
 #define OTH_GREEDY_PLANES 1  // GreedyPolicy on bit planes for N <= 8 (bitboard.hpp OneWord::greedy)
 #endif
@@ -165,6 +171,14 @@ struct Solo {
     static constexpr int RAY_WORDS = 0;
     __device__ __forceinline__ Solo(int, const uint64_t*) {}
     __device__ __forceinline__ BB<Geo<N>::W> legal(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O) const {
+#if OTH_U32 && OTH_SOLO_U32
+        if constexpr (Geo<N>::W == 1) {  // the dword-pair scan (fills unused, so dead)
+            uint64_t t[8];
+            BB<1> r;
+            r.w[0] = OneWord<N>::legal(P.w[0], O.w[0], t);
+            return r;
+        }
+#endif
         return legal_moves<N>(P, O);
     }
     __device__ __forceinline__ BB<Geo<N>::W> flip(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O, int a) const {
@@ -638,6 +652,17 @@ __device__ __forceinline__ int greedy_action(const Lane<N>& s, const Eng& eng) {
         uint64_t t[8];
         (void)OneWord<N>::legal(tw ? s.white.w[0] : s.black.w[0], tw ? s.black.w[0] : s.white.w[0], t);
         return OneWord<N>::greedy(t, s.legal.w[0]);
+    }
+#endif
+#if OTH_GREEDY_PLANES_W
+    // multi-word boards: the same planes on BB<W> (bitboard.hpp PlanesW)
+    if constexpr (is_fills_w<Eng>::value) {
+        return PlanesW<N>::greedy(eng.t, s.legal);  // fills carried from the last scan
+    } else if constexpr (Geo<N>::W > 1) {
+        const bool tw = (s.meta & M_TURN_WHITE) != 0;
+        BB<Geo<N>::W> t[8];
+        (void)legal_moves_fills<N>(pick(tw, s.white, s.black), pick(tw, s.black, s.white), t);
+        return PlanesW<N>::greedy(t, s.legal);
     }
 #endif
     int best, cnt;

@@ -121,7 +121,7 @@ class VecOthelloEnv(object):
         d = dones if dones is not None else self._u8(self.num_envs)
         L.check(self._lib.oth_step(self._h, _ptr(a), _ptr(r), _ptr(d), self._stream()), "oth_step")
         obs = self.get_observation() if observe else None
-        return obs, r, d.bool(), None
+        return obs, r, d.view(torch.bool), None  # 0/1 bytes: a view, not a conversion kernel
 
     def step_policy(self, policy="random", n_plies=1, actions=None, rewards=None, dones=None, record=True):
         """n_plies plies where every board's mover plays `policy` on the device
@@ -171,7 +171,7 @@ class VecOthelloEnv(object):
         r, d, n = self._i32(self.num_envs), self._u8(self.num_envs), self._i32(self.num_envs)
         L.check(self._lib.oth_step_vs(self._h, _POLICIES[opponent], _ptr(a), _ptr(prot), _ptr(r), _ptr(d),
                                       _ptr(n), self._stream()), "oth_step_vs")
-        return (self.get_observation() if observe else None), r, d.bool(), n
+        return (self.get_observation() if observe else None), r, d.view(torch.bool), n
 
     def legal_mask(self):
         """possible_moves of every board as (E, W) int64 bit masks (bit a = square a)."""

@@ -76,6 +76,22 @@ static void fills_flips_n(int E, const uint64_t* mover, const uint64_t* opp, uin
     }
 }
 
+// PlanesW<N>::greedy from legal_moves_fills (multi-word GreedyPolicy on bit planes)
+template <int N>
+static void greedy_planes_w_n(int E, const uint64_t* mover, const uint64_t* opp, const uint64_t* legal, int32_t* out) {
+    constexpr int W = Geo<N>::W;
+    for (int e = 0; e < E; ++e) {
+        BB<W> P, O, L, t[8];
+        for (int i = 0; i < W; ++i) {
+            P.w[i] = mover[e * W + i];
+            O.w[i] = opp[e * W + i];
+            L.w[i] = legal[e * W + i];
+        }
+        (void)legal_moves_fills<N>(P, O, t);
+        out[e] = PlanesW<N>::greedy(t, L);
+    }
+}
+
 #define DISPATCH8(fn, ...)                 \
     switch (n) {                           \
         case 4: fn<4>(__VA_ARGS__); break; \
@@ -115,6 +131,11 @@ int host_flips(int n, int E, const uint64_t* mover, const uint64_t* opp, const i
 }
 int host_fills_flips(int n, int E, const uint64_t* mover, const uint64_t* opp, uint64_t* legal, uint64_t* out) {
     DISPATCH(fills_flips_n, E, mover, opp, legal, out);
+    return 0;
+}
+int host_greedy_planes_w(int n, int E, const uint64_t* mover, const uint64_t* opp, const uint64_t* legal,
+                         int32_t* out) {
+    DISPATCH(greedy_planes_w_n, E, mover, opp, legal, out);
     return 0;
 }
 int host_legal_fills(int n, int E, const uint64_t* mover, const uint64_t* opp, uint64_t* out, uint64_t* fills) {

@@ -32,6 +32,7 @@ def hostlib():
     L.host_legal_fills.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P]
     L.host_greedy_planes.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P]
     L.host_fills_flips.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P]
+    L.host_greedy_planes_w.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P]
     L.host_philox4.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32, P]
     return L
 
@@ -195,3 +196,21 @@ def test_multiword_fills_engine_host_build(hostlib, n):
         assert hostlib.host_flips(n, len(es), ptr(mover[es].copy()), ptr(opp[es].copy()),
                                   ptr(np.array(sqs, dtype=np.int32)), ptr(want)) == 0
         np.testing.assert_array_equal(out[es, sqs], want)
+
+
+@pytest.mark.parametrize("n", [4, 6, 8, 9, 10, 11, 12, 13, 14, 16])
+def test_greedy_planes_multiword_host_build(hostlib, n):
+    """PlanesW<N>::greedy (GreedyPolicy on bit planes for any W, from the
+    fills of legal_moves_fills) plays the oracle's GreedyPolicy move
+    (simple_policies.py:69-92), incl. the lowest-square tie-break and -1
+    without a move."""
+    rng = np.random.RandomState(400 + n)
+    for density in (0.3, 0.6, 0.85, 0.97):
+        _, mover, opp = random_boards(n, 1500, rng, density)
+        s = oracle.State(n, len(mover))
+        s.boards[:] = np.concatenate([mover, opp], axis=1)  # black = mover, black to move
+        s.meta[:] = oracle.meta_from(-np.ones(len(mover)))
+        s.legal[:] = oracle.recompute_legal(s)
+        out = np.zeros(len(mover), dtype=np.int32)
+        assert hostlib.host_greedy_planes_w(n, len(mover), ptr(mover), ptr(opp), ptr(s.legal), ptr(out)) == 0
+        np.testing.assert_array_equal(out, oracle.greedy(s))
