@@ -633,9 +633,9 @@ struct PlanesW {
         }
     }
     static constexpr int min_(int a, int b) { return a < b ? a : b; }
-    // GreedyPolicy.get_action (simple_policies.py:69-92): the candidate of
-    // `legal` flipping the most discs, the lowest of equal counts; -1 without one
-    static OTH_HD int greedy(const BB<W> t[8], const BB<W>& legal) {
+    // the candidates of `legal` with the largest flip count (narrowed plane by
+    // plane from the top) and that count
+    static OTH_HD BB<W> argmax_set(const BB<W> t[8], const BB<W>& legal, int& count) {
         constexpr int K1 = min_(K + 1, T), K2 = min_(K + 2, T);
         BB<W> n[8][K];
         run_len<1>(t[0], n[0]);
@@ -653,16 +653,33 @@ struct PlanesW {
         add<K1, K1, K2>(s1[2], s1[3], s2[1]);
         add<K2, K2, T>(s2[0], s2[1], tot);
         BB<W> cand = legal;
+        int c = 0;
 #pragma unroll
         for (int i = T - 1; i >= 0; --i) {
             const BB<W> h = cand & tot[i];
-            cand = pick(any(h), h, cand);
+            const bool hit = any(h);
+            cand = pick(hit, h, cand);
+            c |= hit ? 1 << i : 0;
         }
+        count = c;
+        return cand;
+    }
+    // GreedyPolicy.get_action (simple_policies.py:69-92): the candidate of
+    // `legal` flipping the most discs, the lowest of equal counts; -1 without one
+    static OTH_HD int greedy(const BB<W> t[8], const BB<W>& legal) {
+        int unused;
+        const BB<W> cand = argmax_set(t, legal, unused);
         int res = -1;
 #pragma unroll
         for (int i = W - 1; i >= 0; --i)
             if (cand.w[i]) res = 64 * i + ctz64(cand.w[i]);
         return res;
+    }
+    // the largest flip count among the candidates of `legal` (0 without one)
+    static OTH_HD int max_flips(const BB<W> t[8], const BB<W>& legal) {
+        int count;
+        (void)argmax_set(t, legal, count);
+        return count;
     }
 };
 

@@ -53,6 +53,9 @@ using namespace oth;
 #ifndef OTH_SOLO_U32
 #define OTH_SOLO_U32 1  // Solo engine (k_step, k_step_vs, ...) scans on dword pairs too for N <= 8
 #endif
+#ifndef OTH_MAXIMIN_PLANES
+#define OTH_MAXIMIN_PLANES 1  // MaxiMin's last search level as the greedy planes' maximum flip count
+#endif
 #ifndef OTH_GREEDY_PLANES_W
 #define OTH_GREEDY_PLANES_W 1  // GreedyPolicy on bit planes for multi-word boards too (bitboard.hpp PlanesW)
 #endif
@@ -697,7 +700,19 @@ __device__ int maximin_node(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O, cons
             const BB<W> P2 = P | f | m;
             const BB<W> O2 = O & ~(f | m);
             int v = popcount(MINE ? P2 : O2);
-            if constexpr (LVL + 1 < D) {
+            if constexpr (LVL + 2 == D && OTH_MAXIMIN_PLANES) {
+                // the child is the last level: its value is the mover's best flip
+                // count over its moves (bit planes, no loop): my discs after the
+                // child's move are O2 + flips + 1 when I move there, P2 - flips otherwise
+                if (any(~(P2 | O2) & Geo<N>::BOARD)) {
+                    BB<W> t2[8];
+                    const BB<W> L2 = legal_moves_fills<N>(O2, P2, t2);
+                    if (any(L2)) {
+                        const int mf = PlanesW<N>::max_flips(t2, L2);
+                        v = ((LVL + 1) % 2 == 0) ? popcount(O2) + 1 + mf : popcount(P2) - mf;
+                    }
+                }
+            } else if constexpr (LVL + 1 < D) {
                 if (any(~(P2 | O2) & Geo<N>::BOARD)) {
                     const BB<W> L2 = legal_moves<N>(O2, P2);
                     if (any(L2)) {

@@ -89,6 +89,7 @@ static void greedy_planes_w_n(int E, const uint64_t* mover, const uint64_t* opp,
         }
         (void)legal_moves_fills<N>(P, O, t);
         out[e] = PlanesW<N>::greedy(t, L);
+        out[E + e] = PlanesW<N>::max_flips(t, L);
     }
 }
 

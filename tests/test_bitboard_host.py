@@ -211,6 +211,15 @@ def test_greedy_planes_multiword_host_build(hostlib, n):
         s.boards[:] = np.concatenate([mover, opp], axis=1)  # black = mover, black to move
         s.meta[:] = oracle.meta_from(-np.ones(len(mover)))
         s.legal[:] = oracle.recompute_legal(s)
-        out = np.zeros(len(mover), dtype=np.int32)
+        out = np.zeros(2 * len(mover), dtype=np.int32)  # [greedy move | its flip count]
         assert hostlib.host_greedy_planes_w(n, len(mover), ptr(mover), ptr(opp), ptr(s.legal), ptr(out)) == 0
-        np.testing.assert_array_equal(out, oracle.greedy(s))
+        g = oracle.greedy(s)
+        np.testing.assert_array_equal(out[:len(mover)], g)
+        # max_flips (MaxiMin's last level): the greedy move's flip count, 0 without a move
+        has = g >= 0
+        f = np.zeros((int(has.sum()), oracle.nwords(n)), dtype=np.uint64)
+        assert hostlib.host_flips(n, int(has.sum()), ptr(mover[has].copy()), ptr(opp[has].copy()),
+                                  ptr(g[has].astype(np.int32)), ptr(f)) == 0
+        cnt = np.array([sum(bin(int(w)).count("1") for w in row) for row in f], dtype=np.int32)
+        np.testing.assert_array_equal(out[len(mover):][has], cnt)
+        assert (out[len(mover):][~has] == 0).all()
