@@ -254,8 +254,7 @@ def main():
         avg_launch_s = kern_ms / 1e3 / launches
         bytes_launch = algorithmic_bytes_per_launch(E, W, P, record)
         achieved = bytes_launch / avg_launch_s / 1e9
-        workload = "random-play-%dx%d-E%d-P%d" % (n, n, E, P) if args.policy == "random" else \
-            "greedy-play-%dx%d-E%d-P%d" % (n, n, E, P)
+        workload = "%s-play-%dx%d-E%d-P%d" % (args.policy, n, n, E, P)
         if not record:
             workload += "-norecord"
         pmc = load_pmc(workload)
