@@ -1,0 +1,64 @@
+"""HIP-graph capture of the device RL loop: masked sampling + step enqueued by
+the C ABI on torch's current stream, captured with torch.cuda.graph and
+replayed, must equal the same plies run eagerly (state, actions, rewards,
+dones, W/D/L) -- the launch-bound single-ply path of ppo.py-style training
+ without per-ply host work.
+
+Graph-safe inputs: caller-supplied uniforms (a captured Philox call counter
+would be frozen at its capture-time value) and initial_rand_steps = 0 (the
+auto-reset opening draw is keyed by the host ply counter)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def _ply(env, logits, u, rew, don, acts_out):
+    act, _, _ = env.sample_actions(logits, uniforms=u, log_probs=False, entropy=False)
+    env.step(act, rewards=rew, dones=don, observe=False)
+    acts_out.copy_(act)
+
+
+@pytest.mark.parametrize("n", [6, 8, 10])
+def test_graph_replay_equals_eager(torch_gpu, n):
+    torch = torch_gpu
+    from gymothelloenv_amd import VecOthelloEnv
+    E, K = 3000, 16
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(n)
+    logits = torch.randn(E, n * n, device=dev, generator=g)
+    u = torch.rand(K, E, device=dev, generator=g)
+    eager = VecOthelloEnv(E, board_size=n, auto_reset=True, seed=9, device=dev)
+    graphed = VecOthelloEnv(E, board_size=n, auto_reset=True, seed=9, device=dev)
+    eager.reset()
+    graphed.reset()
+    rew_e, don_e = torch.empty(K, E, dtype=torch.int32, device=dev), torch.empty(K, E, dtype=torch.uint8, device=dev)
+    rew_g, don_g = torch.empty_like(rew_e), torch.empty_like(don_e)
+    acts_e = torch.empty(K, E, dtype=torch.int32, device=dev)
+    acts_g = torch.empty_like(acts_e)
+
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):  # records only: nothing runs during capture
+        for k in range(K):
+            _ply(graphed, logits, u[k], rew_g[k], don_g[k], acts_g[k])
+    torch.cuda.synchronize()
+    for _ in range(3):  # replays chain: the boards stay in HBM between them
+        for k in range(K):
+            _ply(eager, logits, u[k], rew_e[k], don_e[k], acts_e[k])
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(acts_g, acts_e)
+        assert torch.equal(rew_g, rew_e)
+        assert torch.equal(don_g, don_e)
+        for x, y in zip(graphed.get_state(), eager.get_state()):
+            assert torch.equal(x, y)
+    assert np.array_equal(graphed.counts().cpu().numpy(), eager.counts().cpu().numpy())
+    assert int(eager.counts().sum()) > 0
