@@ -53,6 +53,9 @@ using namespace oth;
 #ifndef OTH_SOLO_U32
 #define OTH_SOLO_U32 1  // Solo engine (k_step, k_step_vs, ...) scans on dword pairs too for N <= 8
 #endif
+#ifndef OTH_TALLY_ATOMIC
+#define OTH_TALLY_ATOMIC 1  // per-block W/D/L slots updated by posted atomics instead of a read-modify-write
+#endif
 #ifndef OTH_MAXIMIN_PLANES
 #define OTH_MAXIMIN_PLANES 1  // MaxiMin's last search level as the greedy planes' maximum flip count
 #endif
@@ -789,9 +792,18 @@ __device__ __forceinline__ void tally(unsigned long long* wdl, uint32_t b, uint3
         }
         if (sb | sd | sw) {
             unsigned long long* slot = wdl + 4 * (size_t)blockIdx.x;
+#if OTH_TALLY_ATOMIC
+            // only this block touches its slot: uncontended atomics without a
+            // return value are posted, so the block does not wait for the slot's
+            // read (the read-modify-write cost one memory round trip per launch)
+            if (sb) atomicAdd(slot + 0, (unsigned long long)sb);
+            if (sd) atomicAdd(slot + 1, (unsigned long long)sd);
+            if (sw) atomicAdd(slot + 2, (unsigned long long)sw);
+#else
             slot[0] += sb;
             slot[1] += sd;
             slot[2] += sw;
+#endif
         }
     }
 #else

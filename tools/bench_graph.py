@@ -20,10 +20,13 @@ def main():
     ap.add_argument("--board-size", type=int, default=8)
     ap.add_argument("--plies", type=int, default=32)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--lib", default=None, help="a variant build (gymothelloenv_amd/variants/liboth_<lib>.so)")
     a = ap.parse_args()
     import torch
 
     from gymothelloenv_amd import VecOthelloEnv
+    from gymothelloenv_amd import _lib as L
+    lib = L.load_path(os.path.join(ROOT, "gymothelloenv_amd", "variants", "liboth_%s.so" % a.lib)) if a.lib else None
     E, n, K = a.envs, a.board_size, a.plies
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
@@ -48,16 +51,16 @@ def main():
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) * 1e3 / (a.reps * K)
 
-    eager = VecOthelloEnv(E, board_size=n, auto_reset=True, seed=0, device=dev)
+    eager = VecOthelloEnv(E, board_size=n, auto_reset=True, seed=0, device=dev, lib=lib)
     eager.reset()
     us_eager = timed(lambda: plies(eager))
-    graphed = VecOthelloEnv(E, board_size=n, auto_reset=True, seed=0, device=dev)
+    graphed = VecOthelloEnv(E, board_size=n, auto_reset=True, seed=0, device=dev, lib=lib)
     graphed.reset()
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(graph):
         plies(graphed)
     us_graph = timed(graph.replay)
-    print(json.dumps({"path": "sample_actions(uniforms) + step", "E": E, "board_size": n, "plies_per_graph": K,
+    print(json.dumps({"path": "sample_actions(uniforms) + step", "lib": a.lib, "E": E, "board_size": n, "plies_per_graph": K,
                       "us_per_ply_eager": us_eager, "us_per_ply_graph": us_graph,
                       "env_steps_per_s_eager": E / (us_eager * 1e-6), "env_steps_per_s_graph": E / (us_graph * 1e-6)}))
 
