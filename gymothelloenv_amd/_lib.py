@@ -54,6 +54,8 @@ SIGNATURES = {
     "oth_sample_actions": (_I32, [_P, _P, _I64, _P, _U64, _I32, _P, _P, _P, _P]),
     "oth_ply_counter": (_U64, [_P]),
     "oth_set_ply_counter": (_I32, [_P, _U64]),
+    "oth_graph_advance": (_I32, [_P, _U64, _U64, _P]),
+    "oth_counter_offsets": (_I32, [_P, _P]),
     "oth_shape": (_I32, [_P, _P, _P, _P]),
     "oth_last_error": (ctypes.c_char_p, []),
     "oth_version": (ctypes.c_char_p, []),

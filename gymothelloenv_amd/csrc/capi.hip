@@ -151,6 +151,8 @@ int oth_create(int32_t n_envs, int32_t board_size, uint32_t flags, uint64_t seed
     const size_t slot_bytes = (size_t)env->nslots * 4 * sizeof(unsigned long long);
     if (err == hipSuccess) err = hipMalloc((void**)&env->wdl, slot_bytes);
     if (err == hipSuccess) err = hipMemset(env->wdl, 0, slot_bytes);
+    if (err == hipSuccess) err = hipMalloc((void**)&env->ctr_off, 2 * sizeof(uint64_t));
+    if (err == hipSuccess) err = hipMemset(env->ctr_off, 0, 2 * sizeof(uint64_t));
     if (err != hipSuccess) {
         oth_destroy(env);
         return hip_fail(err, "oth_create: allocation");
@@ -175,6 +177,7 @@ int oth_destroy(oth_env* env) {
     if (env->meta) (void)hipFree(env->meta);
     if (env->legal) (void)hipFree(env->legal);
     if (env->wdl) (void)hipFree(env->wdl);
+    if (env->ctr_off) (void)hipFree(env->ctr_off);
     delete env;
     return OTH_OK;
 }
@@ -274,15 +277,42 @@ int oth_masked_sample(int32_t board_size, int32_t n, const float* logits, int64_
     if (n < 0 || (n > 0 && (!logits || !legal || !actions))) return fail(OTH_EINVAL, "bad arguments");
     if (ld < (int64_t)bs * bs) return fail(OTH_EINVAL, "ld < board_size^2");
     if (n == 0) return OTH_OK;
-    return launch_masked(bs, n, logits, (long long)ld, legal, uniforms, seed, id_base, counter, mode, actions,
+    return launch_masked(bs, n, logits, (long long)ld, legal, uniforms, seed, id_base, counter, nullptr, mode, actions,
                          log_probs, entropy, (hipStream_t)stream);
 }
 
 int oth_sample_actions(oth_env* env, const float* logits, int64_t ld, const float* uniforms, uint64_t counter,
                        int32_t mode, int32_t* actions, float* log_probs, float* entropy, oth_stream_t stream) {
     OTH_CHECK_ENV(env);
-    return oth_masked_sample(env->n, env->E, logits, ld, env->legal, uniforms, env->seed, env->id_base, counter, mode,
-                             actions, log_probs, entropy, stream);
+    if (!logits || !actions) return fail(OTH_EINVAL, "logits / actions is NULL");
+    if (mode < OTH_MASKED_SAMPLE || mode > OTH_MASKED_EVAL) return fail(OTH_EINVAL, "unknown mode");
+    if (ld < (int64_t)env->n * env->n) return fail(OTH_EINVAL, "ld < N*N");
+    return launch_masked(env->n, env->E, logits, (long long)ld, env->legal, uniforms, env->seed, env->id_base, counter,
+                         env->ctr_off + 1, mode, actions, log_probs, entropy, (hipStream_t)stream);
+}
+
+// The counters' device offsets move on by what one replay of a captured region
+// consumed (enqueued as the region's last node, so every replay advances them).
+__global__ void k_graph_advance(uint64_t* __restrict__ off, uint64_t d_ply, uint64_t d_sample) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        off[0] += d_ply;
+        off[1] += d_sample;
+    }
+}
+
+int oth_graph_advance(oth_env* env, uint64_t d_ply, uint64_t d_sample, oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    hipLaunchKernelGGL(k_graph_advance, dim3(1), dim3(64), 0, (hipStream_t)stream, env->ctr_off, d_ply, d_sample);
+    return oth_host::after_launch("oth_graph_advance");
+}
+
+int oth_counter_offsets(const oth_env* env, uint64_t* out) {
+    OTH_CHECK_ENV(env);
+    if (!out) return fail(OTH_EINVAL, "out is NULL");
+    OTH_HIP(hipSetDevice(env->device));
+    OTH_HIP(hipDeviceSynchronize());
+    OTH_HIP(hipMemcpy(out, env->ctr_off, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return OTH_OK;
 }
 
 int oth_observe(oth_env* env, int32_t layout, int32_t dtype, void* out, oth_stream_t stream) {
@@ -349,6 +379,10 @@ uint64_t oth_ply_counter(const oth_env* env) { return env ? env->ply : 0; }
 int oth_set_ply_counter(oth_env* env, uint64_t ply) {
     if (!env) return fail(OTH_EINVAL, "NULL oth_env");
     env->ply = ply;
+    // the counters are absolute again: drop what graph replays added
+    OTH_HIP(hipSetDevice(env->device));
+    OTH_HIP(hipDeviceSynchronize());
+    OTH_HIP(hipMemset(env->ctr_off, 0, 2 * sizeof(uint64_t)));
     return OTH_OK;
 }
 

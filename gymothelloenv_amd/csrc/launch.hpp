@@ -22,6 +22,7 @@ struct oth_env {
     uint64_t* legal;
     unsigned long long* wdl;  // [nslots][4] per-block W/D/L slots (tally)
     int32_t nslots;
+    uint64_t* ctr_off;  // device [2]: offsets added to the ply counter / the sample counter (graph replays)
 };
 
 namespace oth_host {
@@ -33,8 +34,8 @@ int after_launch(const char* what);
 
 // masked categorical (masked.hip), any board size
 int launch_masked(int n_board, int E, const float* logits, long long ld, const uint64_t* legal, const float* uniforms,
-                  uint64_t seed, uint32_t id_base, uint64_t counter, int mode, int32_t* actions, float* log_probs,
-                  float* entropy, hipStream_t st);
+                  uint64_t seed, uint32_t id_base, uint64_t counter, const uint64_t* counter_off, int mode,
+                  int32_t* actions, float* log_probs, float* entropy, hipStream_t st);
 
 // one set per board size N (kernels_n.hip instantiates them)
 template <int N> int launch_reset(oth_env* env, const uint8_t* mask, hipStream_t st);

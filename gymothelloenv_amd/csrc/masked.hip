@@ -241,9 +241,11 @@ template <int CH, int G, bool VEC, int BPR>
 __global__ __launch_bounds__(MS_BLOCK) void k_masked(int E, int NN, const float* __restrict__ logits, long long ld,
                                                      const uint64_t* __restrict__ legal,
                                                      const float* __restrict__ uniforms, uint64_t seed,
-                                                     uint32_t id_base, uint64_t counter, int mode,
+                                                     uint32_t id_base, uint64_t counter,
+                                                     const uint64_t* __restrict__ counter_off, int mode,
                                                      int32_t* __restrict__ actions, float* __restrict__ log_probs,
                                                      float* __restrict__ entropy) {
+    if (counter_off) counter += *counter_off;  // graph replays advance the device offset (oth_graph_advance)
     const long long t = (long long)blockIdx.x * MS_BLOCK + threadIdx.x;
     const int l = (int)(t % G);
     Slot<CH, G> b[BPR];
@@ -262,16 +264,16 @@ __global__ __launch_bounds__(MS_BLOCK) void k_masked(int E, int NN, const float*
 
 template <int CH, int G, int BPR>
 void launch_ch(bool vec, int E, hipStream_t st, int NN, const float* logits, long long ld, const uint64_t* legal,
-               const float* uniforms, uint64_t seed, uint32_t id_base, uint64_t counter, int mode, int32_t* actions,
-               float* log_probs, float* entropy) {
+               const float* uniforms, uint64_t seed, uint32_t id_base, uint64_t counter, const uint64_t* counter_off,
+               int mode, int32_t* actions, float* log_probs, float* entropy) {
     const long long groups = ((long long)E + BPR - 1) / BPR;
     const int grid = (int)((groups * G + MS_BLOCK - 1) / MS_BLOCK);
     if (vec)
         hipLaunchKernelGGL((k_masked<CH, G, true, BPR>), dim3(grid), dim3(MS_BLOCK), 0, st, E, NN, logits, ld,
-                           legal, uniforms, seed, id_base, counter, mode, actions, log_probs, entropy);
+                           legal, uniforms, seed, id_base, counter, counter_off, mode, actions, log_probs, entropy);
     else
         hipLaunchKernelGGL((k_masked<CH, G, false, BPR>), dim3(grid), dim3(MS_BLOCK), 0, st, E, NN, logits, ld,
-                           legal, uniforms, seed, id_base, counter, mode, actions, log_probs, entropy);
+                           legal, uniforms, seed, id_base, counter, counter_off, mode, actions, log_probs, entropy);
 }
 
 }  // namespace
@@ -279,12 +281,13 @@ void launch_ch(bool vec, int E, hipStream_t st, int NN, const float* logits, lon
 namespace oth_host {
 
 int launch_masked(int n_board, int E, const float* logits, long long ld, const uint64_t* legal, const float* uniforms,
-                  uint64_t seed, uint32_t id_base, uint64_t counter, int mode, int32_t* actions, float* log_probs,
-                  float* entropy, hipStream_t st) {
+                  uint64_t seed, uint32_t id_base, uint64_t counter, const uint64_t* counter_off, int mode,
+                  int32_t* actions, float* log_probs, float* entropy, hipStream_t st) {
     const int NN = n_board * n_board;
     const int CH = (NN + 63) / 64;
     const bool vec = (NN % 4 == 0) && (ld % 4 == 0) && (((uintptr_t)logits & 15u) == 0);
-#define OTH_MS_ARGS vec, E, st, NN, logits, ld, legal, uniforms, seed, id_base, counter, mode, actions, log_probs, entropy
+#define OTH_MS_ARGS \
+    vec, E, st, NN, logits, ld, legal, uniforms, seed, id_base, counter, counter_off, mode, actions, log_probs, entropy
     switch (CH) {  // OTH_MS_G lanes per board up to 128 squares, 16 beyond (registers)
         case 1: launch_ch<1, OTH_MS_G, OTH_MS_BPR>(OTH_MS_ARGS); break;
         case 2: launch_ch<2, OTH_MS_G, 1>(OTH_MS_ARGS); break;

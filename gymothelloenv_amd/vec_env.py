@@ -7,6 +7,7 @@ that stay on the device.  It replaces the reference's CPU "vector env" of one
 process per board (envs.py:7-287) for the hot path; torch here is only device
 memory, streams and the collective for the W/D/L tally.
 """
+import contextlib
 import ctypes
 
 import torch
@@ -278,10 +279,34 @@ class VecOthelloEnv(object):
         self._sample_calls += 1
         return acts, lp, ent
 
+    def counter_offsets(self):
+        """Device offsets graph replays added to (ply counter, sample counter); synchronises."""
+        out = (ctypes.c_uint64 * 2)()
+        L.check(self._lib.oth_counter_offsets(self._h, out), "oth_counter_offsets")
+        return int(out[0]), int(out[1])
+
+    @contextlib.contextmanager
+    def graph_region(self):
+        """Wrap the calls captured into a HIP graph (inside `torch.cuda.graph`):
+        on exit it enqueues oth_graph_advance with what the region consumed of the
+        ply and sample counters, so every replay draws fresh Philox numbers
+        (random openings, the device opponents, sample_actions without uniforms)
+        instead of the capture-time ones.  Eagerly it is a no-op advance by 0.
+
+            with torch.cuda.graph(g), env.graph_region():
+                for k in range(K): env.step(env.sample_actions(actor(obs))[0]); ...
+        """
+        ply0, smp0 = self.ply_counter, self._sample_calls
+        yield self
+        d_ply, d_smp = self.ply_counter - ply0, self._sample_calls - smp0
+        L.check(self._lib.oth_graph_advance(self._h, d_ply, d_smp, self._stream()), "oth_graph_advance")
+
     def state_dict(self):
         b, m, lg = self.get_state()
-        return {"boards": b, "meta": m, "legal": lg, "ply_counter": self.ply_counter,
-                "sample_calls": self._sample_calls, "board_size": self.board_size, "num_envs": self.num_envs}
+        off_ply, off_smp = self.counter_offsets()  # absolute counters, graph replays included
+        return {"boards": b, "meta": m, "legal": lg, "ply_counter": self.ply_counter + off_ply,
+                "sample_calls": self._sample_calls + off_smp, "board_size": self.board_size,
+                "num_envs": self.num_envs}
 
     def load_state_dict(self, sd):
         if sd["board_size"] != self.board_size or sd["num_envs"] != self.num_envs:

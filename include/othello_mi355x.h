@@ -195,9 +195,20 @@ int oth_masked_sample(int32_t board_size, int32_t n, const float *logits, int64_
 int oth_sample_actions(oth_env *env, const float *logits, int64_t ld, const float *uniforms, uint64_t counter,
                        int32_t mode, int32_t *actions, float *log_probs, float *entropy, oth_stream_t stream);
 
-/* Global ply counter of the handle (the Philox counter of the next ply). */
+/* Global ply counter of the handle (the Philox counter of the next ply; host
+ * part, without the graph offset below).  Setting it also zeroes the offsets. */
 uint64_t oth_ply_counter(const oth_env *env);
 int oth_set_ply_counter(oth_env *env, uint64_t ply);
+
+/* HIP-graph support (no reference counterpart: the reference has no device).
+ * Every entry point only enqueues kernels on `stream`, so a region of calls can
+ * be captured and replayed; the Philox counters a capture bakes in (the ply
+ * counter, the sample counter) are offset on the device by out[0] / out[1],
+ * which oth_graph_advance -- enqueued as the region's last call -- moves on by
+ * what one pass of the region consumed, so every replay draws fresh numbers.
+ * Eagerly the offsets stay 0.  oth_counter_offsets synchronises the device. */
+int oth_graph_advance(oth_env *env, uint64_t d_ply, uint64_t d_sample, oth_stream_t stream);
+int oth_counter_offsets(const oth_env *env, uint64_t out[2]);
 
 /* Handle geometry: n_envs, board_size, W. */
 int oth_shape(const oth_env *env, int32_t *n_envs, int32_t *board_size, int32_t *words);

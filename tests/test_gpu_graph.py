@@ -4,9 +4,9 @@ replayed, must equal the same plies run eagerly (state, actions, rewards,
 dones, W/D/L) -- the launch-bound single-ply path of ppo.py-style training
  without per-ply host work.
 
-Graph-safe inputs: caller-supplied uniforms (a captured Philox call counter
-would be frozen at its capture-time value) and initial_rand_steps = 0 (the
-auto-reset opening draw is keyed by the host ply counter)."""
+Plain capture needs caller-supplied uniforms and initial_rand_steps = 0 (the
+Philox counters are host values frozen at capture); VecOthelloEnv.graph_region
+lifts that by advancing device offsets of both counters once per replay."""
 import numpy as np
 import pytest
 
@@ -62,3 +62,49 @@ def test_graph_replay_equals_eager(torch_gpu, n):
             assert torch.equal(x, y)
     assert np.array_equal(graphed.counts().cpu().numpy(), eager.counts().cpu().numpy())
     assert int(eager.counts().sum()) > 0
+
+
+@pytest.mark.parametrize("n", [6, 8])
+def test_graph_region_fresh_draws(torch_gpu, n):
+    """graph_region: device-drawn samples (no uniforms) and random openings
+    (initial_rand_steps > 0) under replay advance the Philox counters on the
+    device, so replay r equals eager plies r*K .. r*K+K-1 of a twin env and two
+    replays draw different actions."""
+    torch = torch_gpu
+    from gymothelloenv_amd import VecOthelloEnv
+    E, K = 2048, 8
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(100 + n)
+    logits = torch.randn(E, n * n, device=dev, generator=g)
+    kw = dict(board_size=n, auto_reset=True, initial_rand_steps=4, seed=5, device=dev)
+    eager, graphed = VecOthelloEnv(E, **kw), VecOthelloEnv(E, **kw)
+    eager.reset()
+    graphed.reset()
+    acts_e = torch.empty(K, E, dtype=torch.int32, device=dev)
+    acts_g = torch.empty_like(acts_e)
+
+    def ply(env, k, out):
+        act, _, _ = env.sample_actions(logits, log_probs=False, entropy=False)
+        env.step(act, observe=False)
+        out[k].copy_(act)
+
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph), graphed.graph_region():
+        for k in range(K):
+            ply(graphed, k, acts_g)
+    torch.cuda.synchronize()
+    prev = None
+    for _ in range(3):
+        for k in range(K):
+            ply(eager, k, acts_e)
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(acts_g, acts_e)
+        for x, y in zip(graphed.get_state(), eager.get_state()):
+            assert torch.equal(x, y)
+        if prev is not None:
+            assert not torch.equal(prev, acts_g)  # fresh draws per replay
+        prev = acts_g.clone()
+    # the device offsets hold what the replays consumed
+    assert graphed.counter_offsets() == (3 * K, 3 * K)
+    assert np.array_equal(graphed.counts().cpu().numpy(), eager.counts().cpu().numpy())
