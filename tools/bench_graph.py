@@ -6,6 +6,7 @@ per-ply wall time on one stream (HIP events), 65,536 8x8 boards by default.
     python tools/bench_graph.py [--envs 65536 --board-size 8 --plies 32 --reps 20]
 """
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -20,6 +21,8 @@ def main():
     ap.add_argument("--board-size", type=int, default=8)
     ap.add_argument("--plies", type=int, default=32)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--device-draws", action="store_true",
+                    help="Philox sampling on the device (no caller uniforms), captured inside env.graph_region()")
     ap.add_argument("--lib", default=None, help="a variant build (gymothelloenv_amd/variants/liboth_<lib>.so)")
     a = ap.parse_args()
     import torch
@@ -37,7 +40,8 @@ def main():
 
     def plies(env):
         for k in range(K):
-            act, _, _ = env.sample_actions(logits, uniforms=u[k], log_probs=False, entropy=False)
+            act, _, _ = env.sample_actions(logits, uniforms=None if a.device_draws else u[k], log_probs=False,
+                                           entropy=False)
             env.step(act, rewards=rew, dones=don, observe=False)
 
     def timed(fn):
@@ -57,10 +61,10 @@ def main():
     graphed = VecOthelloEnv(E, board_size=n, auto_reset=True, seed=0, device=dev, lib=lib)
     graphed.reset()
     graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
+    with torch.cuda.graph(graph), (graphed.graph_region() if a.device_draws else contextlib.nullcontext()):
         plies(graphed)
     us_graph = timed(graph.replay)
-    print(json.dumps({"path": "sample_actions(uniforms) + step", "lib": a.lib, "E": E, "board_size": n, "plies_per_graph": K,
+    print(json.dumps({"path": "sample_actions(%s) + step" % ("device Philox, graph_region" if a.device_draws else "uniforms"), "lib": a.lib, "E": E, "board_size": n, "plies_per_graph": K,
                       "us_per_ply_eager": us_eager, "us_per_ply_graph": us_graph,
                       "env_steps_per_s_eager": E / (us_eager * 1e-6), "env_steps_per_s_graph": E / (us_graph * 1e-6)}))
 
