@@ -108,3 +108,43 @@ def test_graph_region_fresh_draws(torch_gpu, n):
     # the device offsets hold what the replays consumed
     assert graphed.counter_offsets() == (3 * K, 3 * K)
     assert np.array_equal(graphed.counts().cpu().numpy(), eager.counts().cpu().numpy())
+
+
+def test_graph_region_step_vs_random_opponent(torch_gpu):
+    """OthelloEnv-style plies (protagonist action + device random opponent,
+    othello.py:176-200) captured inside graph_region: each replay's opponent
+    draws equal an eager twin's."""
+    torch = torch_gpu
+    from gymothelloenv_amd import VecOthelloEnv
+    E, K, n = 2048, 6, 6
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(7)
+    logits = torch.randn(E, n * n, device=dev, generator=g)
+    kw = dict(board_size=n, auto_reset=True, initial_rand_steps=2, seed=11, device=dev)
+    eager, graphed = VecOthelloEnv(E, **kw), VecOthelloEnv(E, **kw)
+    eager.reset_vs("random")
+    graphed.reset_vs("random")
+    out_e = torch.empty(K, 3, E, dtype=torch.int32, device=dev)
+    out_g = torch.empty_like(out_e)
+
+    def ply(env, k, out):
+        act, _, _ = env.sample_actions(logits, log_probs=False, entropy=False)
+        _, r, d, p = env.step_vs(act, opponent="random", observe=False)
+        out[k, 0].copy_(r)
+        out[k, 1].copy_(d)
+        out[k, 2].copy_(p)
+
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph), graphed.graph_region():
+        for k in range(K):
+            ply(graphed, k, out_g)
+    torch.cuda.synchronize()
+    for _ in range(4):  # 24 calls, about 48 plies: 6x6 games end and auto-reset
+        for k in range(K):
+            ply(eager, k, out_e)
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out_g, out_e)
+        for x, y in zip(graphed.get_state(), eager.get_state()):
+            assert torch.equal(x, y)
+    assert int(out_e[:, 1].sum()) > 0  # games ended in the last replay (auto-reset with random openings)
