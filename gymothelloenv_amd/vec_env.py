@@ -291,13 +291,16 @@ class VecOthelloEnv(object):
         on exit it enqueues oth_graph_advance with what the region consumed of the
         ply and sample counters, so every replay draws fresh Philox numbers
         (random openings, the device opponents, sample_actions without uniforms)
-        instead of the capture-time ones.  Eagerly it is a no-op advance by 0.
+        instead of the capture-time ones.  Outside a capture it enqueues nothing
+        (the host counters already moved on).
 
             with torch.cuda.graph(g), env.graph_region():
                 for k in range(K): env.step(env.sample_actions(actor(obs))[0]); ...
         """
         ply0, smp0 = self.ply_counter, self._sample_calls
         yield self
+        if not torch.cuda.is_current_stream_capturing():
+            return
         d_ply, d_smp = self.ply_counter - ply0, self._sample_calls - smp0
         L.check(self._lib.oth_graph_advance(self._h, d_ply, d_smp, self._stream()), "oth_graph_advance")
 

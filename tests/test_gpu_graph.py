@@ -95,8 +95,9 @@ def test_graph_region_fresh_draws(torch_gpu, n):
     torch.cuda.synchronize()
     prev = None
     for _ in range(3):
-        for k in range(K):
-            ply(eager, k, acts_e)
+        with eager.graph_region():  # outside a capture: enqueues nothing
+            for k in range(K):
+                ply(eager, k, acts_e)
         graph.replay()
         torch.cuda.synchronize()
         assert torch.equal(acts_g, acts_e)
@@ -107,6 +108,7 @@ def test_graph_region_fresh_draws(torch_gpu, n):
         prev = acts_g.clone()
     # the device offsets hold what the replays consumed
     assert graphed.counter_offsets() == (3 * K, 3 * K)
+    assert eager.counter_offsets() == (0, 0)
     assert np.array_equal(graphed.counts().cpu().numpy(), eager.counts().cpu().numpy())
 
 
