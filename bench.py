@@ -1,29 +1,42 @@
 #!/usr/bin/env python3
-"""Benchmark: env-steps/s of on-device random play on 65,536 8x8 boards per GPU
-(BASELINE.json `metric`, config 2; N GPUs = config 4's weak-scaled shards).
+"""Benchmark: env-steps/s of on-device random play on 8x8 boards (BASELINE.json
+`metric`; config 2 at one GPU, config 4's shards at N GPUs).
 
-A step = one ply applied to every board of the shard (one OthelloBaseEnv.step
-per board, pass resolution included), the mover choosing uniformly among its
-possible_moves (RandomPolicy, simple_policies.py:37-41) from a Philox stream;
-finished games auto-reset.  Boards, actions, rewards and dones stay in HBM.
-`--plies-per-launch P` runs P plies per kernel launch (board state kept in
-registers between plies, every ply's action / reward / done still stored).
+Units:
+  * env-step = one ply applied to one board (one OthelloBaseEnv.step,
+    othello.py:412-462, pass resolution included); the mover
+    picks uniformly among its possible_moves (RandomPolicy,
+    simple_policies.py:37-41) from a Philox stream; finished games auto-reset.
+  * bench step = one rollout segment: `--plies-per-step` P (default 100) plies
+    over every board of the shard, one k_play launch (boards kept in registers
+    between plies; every ply's action / reward / done stored to HBM).
+`--steps K --warmup W` run exactly W untimed and K timed bench steps.
 
     python bench.py [--gpus N --steps K --warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU, RCCL)
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts the N
+ranks itself (one process per GPU, RANK / LOCAL_RANK / WORLD_SIZE set, before
+the parent touches the GPU) and exits with their status.  Boards per GPU:
+65,536 at one GPU (config 2), 131,072 at N > 1 (config 4: 1,048,576 over 8);
+`--envs` / `--global-envs` override.  Boards are sharded by global env id
+(ShardedVecOthelloEnv); the only exchange is the W/D/L all-gather (RCCL).
 
 Rank 0 prints one JSON line.  `roofline` prices the dominant kernel
-(k_play<8, random>) by its algorithmic HBM bytes per launch over its average
-launch time (HIP events on the launch stream); `traffic` comes from the
-rocprofv3 PMC summary committed under profiles/ (null if absent).
-`cpu_baseline` times the oracle's scalar restatement of othello.py on the
-host cores (one batch of boards per thread) over a bounded sample.
-`masked_sample` is a side measurement of the learners' masked-categorical
-kernel against the HBM peak.
+(k_play<8, random>) at SURVEY.md §8(d)'s algorithmic bytes per env-step
+(40W + 11 = 51 B at 8x8) x env-steps per launch over its average launch time
+(HIP events on the launch stream); `traffic` is the measured HBM bytes per
+launch from the rocprofv3 PMC summary committed under profiles/; the kernel's
+binding limit is integer VALU issue (`valu`).  `cpu_baseline` times the
+bitboard CPU engine (oracle/cpu_bitboard.cpp: the kernels' rules templates
+compiled for the host) and the scalar restatement of othello.py's ray walk
+(oracle/othello_oracle.c) on the host cores over bounded samples.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -31,16 +44,24 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-METRIC = "env-steps/sec (random policy, 65,536\u00d78\u00d78 boards) at 1/2/4/8 GPUs; HBM GB/s vs peak"
+# VALU issue peak: 256 CUs x 4 SIMDs x one wave64 instruction per 2 cycles at 2.4 GHz
+VALU_PEAK_WAVE_INSTS = 256 * 4 * 2.4e9 / 2
+METRIC = "env-steps/sec (random policy, 65,536×8×8 boards) at 1/2/4/8 GPUs; HBM GB/s vs peak"
+CONFIG2_BOARDS = 65536
+CONFIG4_BOARDS_PER_GPU = 131072
 
 
-def algorithmic_bytes_per_launch(E, W, plies, record=True):
-    """HBM bytes one k_play launch must move: board state in and out once
-    (boards 16W + legal 8W + meta 2, each way) plus per ply the action (4),
-    reward (4) and done (1) of every board."""
-    state = 2 * (16 * W + 8 * W + 2)
-    per_ply = (4 + 4 + 1) if record else 0
-    return E * (state + plies * per_ply)
+def step_bytes(W):
+    """algorithmic HBM bytes per env-step, 40W + 11 (51 at W = 1):
+    state 16W + flags 1 + action 4 in; state 16W + flags 1 + legal 8W + reward 4 + done 1 out."""
+    return 40 * W + 11
+
+
+def fused_bytes_per_launch(E, W, plies, record=True):
+    """HBM bytes one fused k_play launch moves: the board state in and out once
+    (boards 16W + legal 8W + meta 2, each way) plus per ply action (4), reward (4)
+    and done (1) of every board.  Compare with the PMC `traffic`."""
+    return E * (2 * (16 * W + 8 * W + 2) + plies * ((4 + 4 + 1) if record else 0))
 
 
 def cpu_threads():
@@ -51,88 +72,179 @@ def cpu_threads():
     return max(1, min(n, int(cap))) if cap and cap.isdigit() else n
 
 
-def cpu_baseline(seconds, board_size=8, threads=None):
-    """Scalar restatement of the reference rules engine (oracle/, the per-cell
-    8-direction ray walk of othello.py:273-343) with the same random policy and
-    auto-reset, one independent batch of boards per host thread (the ctypes
-    call releases the GIL); a bounded sample of about `seconds` CPU-seconds
-    (at least 2 s of wall time)."""
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _timed_threads(T, wall, work):
+    """Run work(k, deadline_fn) on T threads started together; returns
+    (sum of env-steps, max seconds)."""
     import concurrent.futures
     import threading
-
-    from oracle import oracle
-    T = threads or cpu_threads()
-    E, chunk = 1024, 16
-    wall = max(2.0, seconds / T)
-    flags = oracle.F_SUDDEN_DEATH | oracle.F_AUTO_RESET
     start = threading.Barrier(T + 1)
 
     def worker(k):
-        s = oracle.reset(board_size, E)
-        plies = 0
         start.wait()
         t0 = time.perf_counter()
-        while time.perf_counter() - t0 < wall:
-            oracle.rollout(s, flags, 0, chunk, seed=0, id_base=k * E, ply0=plies, record=False)
-            plies += chunk
-        return plies, time.perf_counter() - t0
+        steps = work(k, lambda: time.perf_counter() - t0 < wall)
+        return steps, time.perf_counter() - t0
 
     with concurrent.futures.ThreadPoolExecutor(T) as ex:
         futs = [ex.submit(worker, k) for k in range(T)]
         start.wait()
         res = [f.result() for f in futs]
-    steps = sum(E * p for p, _ in res)
-    dt = max(t for _, t in res)
-    return {"value": steps / dt, "unit": "env-steps/s", "cores": T, "kind": "port",
-            "per_core": steps / dt / T,
-            "sample": "%d threads x %d boards of random play, %dx%d, auto-reset, %d env-steps in %.1f s: "
-                      "oracle/othello_oracle.c scalar ray-scan restatement of othello.py (same per-cell "
-                      "8-direction walk as the reference), one batch per thread"
-                      % (T, E, board_size, board_size, steps, dt)}
+    return sum(s for s, _ in res), max(t for _, t in res)
 
 
-# VALU issue peak: 256 CUs x 4 SIMD32 x one wave64 instruction per 2 cycles at 2.4 GHz
-VALU_PEAK_WAVE_INSTS = 256 * 4 * 2.4e9 / 2
+def cpu_baseline(seconds, board_size=8, threads=None):
+    """Two CPU engines on the host cores, one independent batch of boards per
+    thread (ctypes calls release the GIL), each a bounded sample of about
+    `seconds` CPU-seconds (at least 2 s of wall time):
+      * bitboard (the headline CPU figure, "best CPU" of SURVEY.md §8(d)):
+        oracle/cpu_bitboard.cpp, the kernels' shift/mask rules compiled with g++;
+      * scalar port: oracle/othello_oracle.c, the per-cell 8-direction ray walk
+        of othello.py:273-343 (the reference's algorithm).
+    Both play random moves from the device's Philox stream with auto-reset."""
+    from oracle import oracle
+    T = threads or cpu_threads()
+    wall = max(2.0, seconds / T)
+    flags = oracle.F_SUDDEN_DEATH | oracle.F_AUTO_RESET
+    E, chunk = 1024, 16
+
+    def bb_work(k, more):
+        s, steps, ply = oracle.reset(board_size, E), 0, 0
+        while more():
+            steps += oracle.bb_rollout(s, chunk, id_base=k * E, ply0=ply, record=False)[4]
+            ply += chunk
+        return steps
+
+    def scalar_work(k, more):
+        s, ply = oracle.reset(board_size, E), 0
+        while more():
+            oracle.rollout(s, flags, 0, chunk, seed=0, id_base=k * E, ply0=ply, record=False)
+            ply += chunk
+        return E * ply
+
+    bb_steps, bb_dt = _timed_threads(T, wall, bb_work)
+    sc_steps, sc_dt = _timed_threads(T, wall, scalar_work)
+    model = cpu_model()
+    return {"value": bb_steps / bb_dt, "unit": "env-steps/s", "cores": T, "kind": "port",
+            "per_core": bb_steps / bb_dt / T, "cpu_model": model,
+            "sample": "%d threads x %d boards of random play, %dx%d, auto-reset, %d env-steps in %.1f s on %s: "
+                      "oracle/cpu_bitboard.cpp (bitboard.hpp's shift/mask rules compiled for the host, g++ -O3), "
+                      "one batch per thread" % (T, E, board_size, board_size, bb_steps, bb_dt, model),
+            "scalar_port": {"value": sc_steps / sc_dt, "unit": "env-steps/s", "cores": T, "kind": "port",
+                            "per_core": sc_steps / sc_dt / T,
+                            "sample": "%d threads x %d boards, %d env-steps in %.1f s: oracle/othello_oracle.c "
+                                      "scalar ray-scan restatement of othello.py:273-343" % (T, E, sc_steps, sc_dt)}}
 
 
 def load_pmc(workload):
     """The rocprofv3 PMC summary of this workload committed under profiles/
     (tools/pmc_profile.sh + tools/pmc_summarize.py), or None."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(p):
-        return None
     try:
         return json.load(open(p)).get(workload)
     except Exception:
         return None
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2000)
-    ap.add_argument("--warmup", type=int, default=200)
-    ap.add_argument("--envs", type=int, default=65536, help="boards per GPU")
+    ap.add_argument("--steps", type=int, default=50, help="timed bench steps (rollout segments)")
+    ap.add_argument("--warmup", type=int, default=10, help="untimed bench steps")
+    ap.add_argument("--plies-per-step", type=int, default=None,
+                    help="plies per bench step = per k_play launch (default 100 random, 10 otherwise)")
+    ap.add_argument("--envs", type=int, default=None, help="boards per GPU")
+    ap.add_argument("--global-envs", type=int, default=None, help="boards over all GPUs")
     ap.add_argument("--board-size", type=int, default=8)
     ap.add_argument("--policy", default="random", choices=["random", "greedy", "maximin1", "maximin2", "maximin3"])
-    ap.add_argument("--plies-per-launch", type=int, default=None)
     ap.add_argument("--no-record", action="store_true", help="do not store per-ply action/reward/done")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-single-ply", action="store_true", help="skip the one-ply-per-launch side measurement")
-    ap.add_argument("--no-masked", action="store_true", help="skip the masked-categorical side measurement")
-    args = ap.parse_args()
+    ap.add_argument("--no-side", action="store_true", help="skip the side measurements")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="ranks, process group and shard plan only (no GPU call); for CPU tests")
+    return ap.parse_args(argv)
+
+
+def plan(args, world, rank):
+    """Boards of this rank: (global_envs, env_id_base, n_local, plies per step)."""
+    if args.global_envs is not None and args.envs is not None:
+        raise SystemExit("give --envs or --global-envs, not both")
+    if args.global_envs is not None:
+        G = args.global_envs
+    else:
+        per = args.envs if args.envs is not None else (CONFIG2_BOARDS if world == 1 else CONFIG4_BOARDS_PER_GPU)
+        G = per * world
+    from gymothelloenv_amd.distributed import shard
+    base, n_local = shard(G, world, rank)
+    if n_local <= 0:
+        raise SystemExit("rank %d has no boards (global %d over %d ranks)" % (rank, G, world))
+    P = args.plies_per_step or (100 if args.policy == "random" else 10)
+    if args.steps <= 0 or args.warmup < 0 or P <= 0:
+        raise SystemExit("need --steps > 0, --warmup >= 0, --plies-per-step > 0")
+    return G, base, n_local, P
+
+
+def spawn(argv, n):
+    """Start n ranks of this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*
+    set) without touching the GPU here; return the first non-zero exit status."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn(argv, args.gpus)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print("bench.py: WORLD_SIZE=%d but --gpus %d" % (world, args.gpus), file=sys.stderr)
+        return 2
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    G, base, E, P = plan(args, world, rank)
 
     import torch
     import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # test hooks for rehearsing the multi-process path on a one-GPU box:
-    # OTH_BENCH_DEVICE pins every rank to one device, OTH_BENCH_BACKEND=gloo
-    gpu = int(os.environ.get("OTH_BENCH_DEVICE", local))
+    # test hooks: OTH_BENCH_BACKEND=gloo (CPU tests, or rehearsing N ranks on one
+    # GPU), OTH_BENCH_DEVICE pins every rank to one device
     backend = os.environ.get("OTH_BENCH_BACKEND", "nccl")
+    gpu = int(os.environ.get("OTH_BENCH_DEVICE", local))
+    if args.dry_run:
+        if world > 1:
+            dist.init_process_group("gloo")
+            mine = torch.tensor([rank, base, E], dtype=torch.int64)
+            parts = [torch.empty_like(mine) for _ in range(world)]
+            dist.all_gather(parts, mine)
+            rows = [p.tolist() for p in parts]
+            dist.destroy_process_group()
+        else:
+            rows = [[rank, base, E]]
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "world": world, "global_envs": G, "plies_per_step": P,
+                              "shards": rows}), flush=True)
+        return 0
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
@@ -141,30 +253,25 @@ def main():
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
 
-    from gymothelloenv_amd import VecOthelloEnv
-    from gymothelloenv_amd.distributed import gather_wdl, shard
+    from gymothelloenv_amd.distributed import ShardedVecOthelloEnv, gather_wdl
     from gymothelloenv_amd.vec_env import nwords
 
-    E, n = args.envs, args.board_size
+    n = args.board_size
     W = nwords(n)
-    P = args.plies_per_launch or (100 if args.policy == "random" else 10)
-    steps = max(P, (args.steps // P) * P)
-    warm = max(P, (args.warmup // P) * P) if args.warmup > 0 else 0
-    launches = steps // P
     record = not args.no_record
-    base, _ = shard(E * world, world, rank)  # weak scaling: E boards per GPU, global ids rank*E ...
-    env = VecOthelloEnv(E, board_size=n, auto_reset=True, seed=0, env_id_base=base,
-                        initial_rand_steps=10 if args.policy == "greedy" else 0, device=dev)
+    env = ShardedVecOthelloEnv(G, rank=rank, world=world, board_size=n, auto_reset=True, seed=0,
+                               initial_rand_steps=10 if args.policy == "greedy" else 0, device=dev)
+    assert env.num_envs == E and env.env_id_base == base
     env.reset()
     acts = torch.empty(P, E, dtype=torch.int32, device=dev) if record else None
     rews = torch.empty(P, E, dtype=torch.int32, device=dev) if record else None
     dns = torch.empty(P, E, dtype=torch.uint8, device=dev) if record else None
 
-    def run(k_launches):
-        for _ in range(k_launches):
+    def run(k):
+        for _ in range(k):
             env.step_policy(args.policy, n_plies=P, actions=acts, rewards=rews, dones=dns, record=record)
 
-    run(warm // P)
+    run(args.warmup)
     env.counts(reset=True)
     torch.cuda.synchronize()
     if world > 1:
@@ -174,7 +281,7 @@ def main():
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
-    run(launches)
+    run(args.steps)
     ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -183,119 +290,137 @@ def main():
     wall = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1)  # HIP events on the launch stream
     wdl = env.counts()
-    t = torch.tensor([wall], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
     if world > 1:
+        t = torch.tensor([wall], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall_max = float(t.item())
         wdl_total = gather_wdl(wdl).sum(0)  # RCCL all-gather over xGMI: the W/D/L tally
     else:
-        wdl_total = wdl
-    wall_max = float(t.item())
+        wall_max, wdl_total = wall, wdl
     wdl_total = [int(x) for x in wdl_total.cpu().tolist()]
 
-    # the same play one ply per launch: every ply's state round-trips HBM (the
-    # north-star kernel shape); reported beside the headline, not as `value`
-    single = None
-    if not args.no_single_ply and world == 1:
-        a1 = torch.empty(1, E, dtype=torch.int32, device=dev)
-        r1 = torch.empty(1, E, dtype=torch.int32, device=dev)
-        d1 = torch.empty(1, E, dtype=torch.uint8, device=dev)
-        for _ in range(50):
-            env.step_policy(args.policy, n_plies=1, actions=a1, rewards=r1, dones=d1)
-        torch.cuda.synchronize()
-        k1 = 500
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(k1):
-            env.step_policy(args.policy, n_plies=1, actions=a1, rewards=r1, dones=d1)
-        e1.record(stream)
-        torch.cuda.synchronize()
-        us = e0.elapsed_time(e1) * 1e3 / k1
-        b1 = algorithmic_bytes_per_launch(E, W, 1, True)
-        single = {"value": E / (us * 1e-6), "unit": "env-steps/s", "avg_launch_us": us,
-                  "algorithmic_bytes_per_launch": b1, "achieved_GBps": b1 / (us * 1e-6) / 1e9,
-                  "steps": k1}
-
-    # side measurement: the learners' masked categorical (csrc/masked.hip) over
-    # 4,194,304 boards' fp32 logits (1.1 GB: beyond the 256 MiB Infinity Cache)
-    masked = None
-    if not args.no_masked and world == 1:
-        from gymothelloenv_amd import masked_sample
-        Em, nn = 4194304, n * n
-        g = torch.Generator(device=dev).manual_seed(0)
-        logits = torch.randn(Em, nn, device=dev, generator=g)
-        legal = env.legal_mask().repeat((Em + E - 1) // E, 1)[:Em].contiguous()
-        outs = [torch.empty(Em, dtype=torch.int32, device=dev)] + \
-            [torch.empty(Em, dtype=torch.float32, device=dev) for _ in range(2)]
-        lib = env._lib
-        import ctypes
-        args_m = lambda c: (n, Em, ctypes.c_void_p(logits.data_ptr()), nn, ctypes.c_void_p(legal.data_ptr()),
-                            None, 0, 0, c, 0, *[ctypes.c_void_p(o.data_ptr()) for o in outs],
-                            ctypes.c_void_p(stream.cuda_stream))
-        for c in range(3):
-            lib.oth_masked_sample(*args_m(c))
-        torch.cuda.synchronize()
-        km = 20
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for c in range(km):
-            lib.oth_masked_sample(*args_m(c))
-        e1.record(stream)
-        torch.cuda.synchronize()
-        us = e0.elapsed_time(e1) * 1e3 / km
-        bm = Em * (4 * nn + 8 * W + 12)
-        masked = {"kernel": "k_masked", "boards": Em, "avg_launch_us": us, "algorithmic_bytes_per_launch": bm,
-                  "achieved_GBps": bm / (us * 1e-6) / 1e9, "frac_hbm_peak": bm / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS,
-                  "boards_per_s": Em / (us * 1e-6)}
-        del logits, legal, outs
+    side = {}
+    if not args.no_side and world == 1 and rank == 0:
+        side = side_measurements(env.env, args.policy, E, n, W, dev, stream)
 
     if rank == 0:
-        total_steps = E * world * steps
-        value = total_steps / wall_max
-        avg_launch_s = kern_ms / 1e3 / launches
-        bytes_launch = algorithmic_bytes_per_launch(E, W, P, record)
-        achieved = bytes_launch / avg_launch_s / 1e9
+        env_steps = G * P * args.steps
+        avg_launch_s = kern_ms / 1e3 / args.steps
+        bps = step_bytes(W)
+        alg_launch = E * P * bps
+        achieved = alg_launch / avg_launch_s / 1e9
         workload = "%s-play-%dx%d-E%d-P%d" % (args.policy, n, n, E, P)
         if not record:
             workload += "-norecord"
         pmc = load_pmc(workload)
+        valu = None
+        if pmc and pmc.get("valu_insts_per_launch"):
+            rate = pmc["valu_insts_per_launch"] / avg_launch_s
+            valu = {"achieved_wave_insts_per_s": rate, "peak_wave_insts_per_s": VALU_PEAK_WAVE_INSTS,
+                    "frac": rate / VALU_PEAK_WAVE_INSTS,
+                    "insts_per_board_ply": pmc["valu_insts_per_launch"] / (E * P),
+                    "source": "SQ_INSTS_VALU per launch from profiles/pmc_traffic.json, this run's launch time"}
+        if args.policy == "random":
+            metric = METRIC
+        else:
+            metric = "env-steps/sec (%s policy on device, %dx%d)" % (args.policy, n, n)
+        config_name = "config2" if (world == 1 and G == CONFIG2_BOARDS) else \
+            ("config4" if (world == 8 and G == 8 * CONFIG4_BOARDS_PER_GPU) else "custom")
         out = {
-            "metric": METRIC if args.policy == "random" else "env-steps/sec (%s policy on device)" % args.policy,
-            "value": value,
+            "metric": metric,
+            "value": env_steps / wall_max,
             "unit": "env-steps/s",
             "n_gpus": world,
-            "steps": steps,
-            "warmup": warm,
-            "ms_per_step": wall_max / steps * 1e3,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": wall_max / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic (standard opening, Philox random play, auto-reset)",
-            "config": {"workload": workload, "boards_per_gpu": E, "board_size": n,
-                       "global_boards": E * world, "plies_per_launch": P, "policy": args.policy,
-                       "per_ply_outputs_stored": record, "parallelism": "dp%d (independent shards)" % world},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "config": {"workload": workload, "baseline_config": config_name, "boards_per_gpu": E,
+                       "global_boards": G, "board_size": n, "plies_per_step": P,
+                       "env_steps_per_step": G * P, "policy": args.policy, "per_ply_outputs_stored": record,
+                       "parallelism": "dp%d (independent shards, W/D/L all-gather only)" % world},
+            "roofline": {"bound": "valu-issue", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS,
                          "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
                          "kernel": "k_play<%d,%s>" % (n, args.policy), "avg_launch_us": avg_launch_s * 1e6,
-                         "algorithmic_bytes_per_launch": bytes_launch,
-                         "valu": None if not pmc or not pmc.get("valu_insts_per_launch") else {
-                             "achieved_wave_insts_per_s": pmc["valu_insts_per_launch"] / avg_launch_s,
-                             "peak_wave_insts_per_s": VALU_PEAK_WAVE_INSTS,
-                             "frac": pmc["valu_insts_per_launch"] / avg_launch_s / VALU_PEAK_WAVE_INSTS,
-                             "note": "the kernel's real limiter: integer VALU issue (one wave per SIMD at "
-                                     "65,536 boards), see DESIGN.md"}},
+                         "launches_timed": args.steps,
+                         "algorithmic_bytes_per_env_step": bps,
+                         "algorithmic_bytes_per_launch": alg_launch,
+                         "fused_bytes_per_launch": fused_bytes_per_launch(E, W, P, record),
+                         "valu": valu,
+                         "note": "achieved/frac: SURVEY §8(d) bytes (40W+11 per env-step); traffic: PMC "
+                                 "FETCH_SIZE x2 + WRITE_SIZE per launch (the fused kernel keeps boards in "
+                                 "registers between plies); the limiter is integer VALU issue"},
             "wdl": {"black_wins": wdl_total[0], "draws": wdl_total[1], "white_wins": wdl_total[2]},
-            "single_ply_launches": single,
-            "masked_sample": masked,
         }
+        out.update(side)
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, n)
         print(json.dumps(out), flush=True)
     env.close()
     if world > 1:
         dist.destroy_process_group()
+    return 0
+
+
+def side_measurements(env, policy, E, n, W, dev, stream):
+    """Beside the headline (never `value`): one ply per launch (the north-star
+    per-step shape: state through HBM every ply) and the learners' masked
+    categorical over 4,194,304 boards' fp32 logits (beyond the 256 MiB MALL)."""
+    import ctypes
+
+    import torch
+    out = {}
+    a1 = torch.empty(1, E, dtype=torch.int32, device=dev)
+    r1 = torch.empty(1, E, dtype=torch.int32, device=dev)
+    d1 = torch.empty(1, E, dtype=torch.uint8, device=dev)
+    for _ in range(50):
+        env.step_policy(policy, n_plies=1, actions=a1, rewards=r1, dones=d1)
+    torch.cuda.synchronize()
+    k1 = 500
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(k1):
+        env.step_policy(policy, n_plies=1, actions=a1, rewards=r1, dones=d1)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / k1
+    out["single_ply_launches"] = {"value": E / (us * 1e-6), "unit": "env-steps/s", "avg_launch_us": us,
+                                  "algorithmic_GBps": E * step_bytes(W) / (us * 1e-6) / 1e9, "launches": k1}
+
+    Em, nn = 4194304, n * n
+    g = torch.Generator(device=dev).manual_seed(0)
+    logits = torch.randn(Em, nn, device=dev, generator=g)
+    legal = env.legal_mask().repeat((Em + E - 1) // E, 1)[:Em].contiguous()
+    outs = [torch.empty(Em, dtype=torch.int32, device=dev)] + \
+        [torch.empty(Em, dtype=torch.float32, device=dev) for _ in range(2)]
+    lib = env._lib
+
+    def call(c):
+        lib.oth_masked_sample(n, Em, ctypes.c_void_p(logits.data_ptr()), nn, ctypes.c_void_p(legal.data_ptr()),
+                              None, 0, 0, c, 0, *[ctypes.c_void_p(o.data_ptr()) for o in outs],
+                              ctypes.c_void_p(stream.cuda_stream))
+    for c in range(3):
+        call(c)
+    torch.cuda.synchronize()
+    km = 20
+    e0.record(stream)
+    for c in range(km):
+        call(c)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / km
+    bm = Em * (4 * nn + 8 * W + 12)
+    out["masked_sample"] = {"kernel": "k_masked", "boards": Em, "avg_launch_us": us,
+                            "algorithmic_bytes_per_launch": bm, "achieved_GBps": bm / (us * 1e-6) / 1e9,
+                            "frac_hbm_peak": bm / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS}
+    del logits, legal, outs
+    return out
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -79,6 +79,12 @@ def load(require_gpu=True):
             raise OthelloLibError(
                 "%s not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
                 "(hipcc --offload-arch=gfx950); there is no CPU fallback" % LIB_PATH)
+        from . import build as _build
+        have, want = _build.embedded_hash(LIB_PATH), _build.source_hash()
+        if have != want:
+            raise OthelloLibError(
+                "%s was built from other sources (embedded %s, tree %s): rebuild it with "
+                "`python -m gymothelloenv_amd.build`" % (LIB_PATH, (have or "none")[:16], want[:16]))
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(lib, name)

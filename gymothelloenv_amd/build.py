@@ -3,30 +3,60 @@ travels with the repo snapshot to the GPU box).
 
 The kernels are templates over the board size N; csrc/kernels_n.hip is
 compiled once per N (-DOTH_N=4..16) in parallel, csrc/capi.hip holds the C
-ABI, and the objects are linked into one shared library."""
+ABI, and the objects are linked into one shared library.
+
+Reproducibility: objects go to a fixed directory (`_objs/`, git-ignored) so the
+compiler's per-TU ids (derived from the input path and options) are the same on
+every build, and the library embeds the SHA-256 of its sources and flags
+(`oth_version()` reports it, `embedded_hash()` reads it from the file).  The
+loader refuses a library whose embedded hash is not the hash of the sources in
+the tree, so a binary that ran on the GPU box is provably built from HEAD."""
 import concurrent.futures
+import hashlib
 import os
+import re
 import shutil
 import subprocess
 import sys
-import tempfile
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 SIZES = list(range(4, 17))
-DEPS = [os.path.join(CSRC, f) for f in ("capi.hip", "kernels_n.hip", "masked.hip", "device.hpp", "launch.hpp", "bitboard.hpp")] + \
-    [os.path.join(ROOT, "include", "othello_mi355x.h")]
+SOURCES = ("capi.hip", "kernels_n.hip", "masked.hip", "device.hpp", "launch.hpp", "bitboard.hpp")
+DEPS = [os.path.join(CSRC, f) for f in SOURCES] + [os.path.join(ROOT, "include", "othello_mi355x.h")]
 OUT = os.path.join(HERE, "liboth_mi355x.so")
+OBJDIR = os.path.join(HERE, "_objs")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("OTH_OFFLOAD_ARCH", "gfx950")
+BASE_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-pass-failed"]
+_HASH_RE = re.compile(rb"oth-src-sha256:([0-9a-f]{64})")
 
 
-def needs_build(out=OUT):
-    if not os.path.exists(out):
-        return True
-    t = os.path.getmtime(out)
-    return any(os.path.getmtime(p) > t for p in DEPS)
+def source_hash(extra_flags=()):
+    """SHA-256 over the library's sources (name + bytes) and its build flags."""
+    h = hashlib.sha256()
+    for p in DEPS:
+        h.update(os.path.basename(p).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    h.update(" ".join([ARCH] + BASE_FLAGS + list(extra_flags)).encode())
+    return h.hexdigest()
+
+
+def embedded_hash(path=OUT):
+    """The source hash a built library carries (None if absent or unreadable)."""
+    try:
+        with open(path, "rb") as f:
+            m = _HASH_RE.search(f.read())
+    except OSError:
+        return None
+    return m.group(1).decode() if m else None
+
+
+def needs_build(out=OUT, extra_flags=()):
+    return embedded_hash(out) != source_hash(extra_flags)
 
 
 def _jobs():
@@ -36,12 +66,14 @@ def _jobs():
 
 
 def build(force=False, verbose=True, extra_flags=(), out=OUT, jobs=None):
-    if not force and not needs_build(out):
+    if not force and not needs_build(out, extra_flags):
         return out
-    objdir = tempfile.mkdtemp(prefix="oth_objs_")
-    base = [HIPCC, "--offload-arch=%s" % ARCH, "-O3", "-std=c++17", "-fPIC", "-Wall",
-            "-Wno-pass-failed", "-I", os.path.join(ROOT, "include")] + list(extra_flags)
-    units = [(os.path.join(CSRC, "capi.hip"), os.path.join(objdir, "capi.o"), []),
+    digest = source_hash(extra_flags)
+    objdir = OBJDIR if out == OUT else os.path.join(OBJDIR, os.path.splitext(os.path.basename(out))[0])
+    shutil.rmtree(objdir, ignore_errors=True)
+    os.makedirs(objdir)
+    base = [HIPCC, "--offload-arch=%s" % ARCH] + BASE_FLAGS + ["-I", os.path.join(ROOT, "include")] + list(extra_flags)
+    units = [(os.path.join(CSRC, "capi.hip"), os.path.join(objdir, "capi.o"), ['-DOTH_SRC_HASH="%s"' % digest]),
              (os.path.join(CSRC, "masked.hip"), os.path.join(objdir, "masked.o"), [])]
     units += [(os.path.join(CSRC, "kernels_n.hip"), os.path.join(objdir, "kernels_n%d.o" % n), ["-DOTH_N=%d" % n])
               for n in SIZES]
@@ -49,20 +81,17 @@ def build(force=False, verbose=True, extra_flags=(), out=OUT, jobs=None):
     def compile_one(u):
         src, obj, defs = u
         cmd = base + defs + ["-c", "-o", obj, src]
-        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, cwd=ROOT)
         if r.returncode != 0:
             raise RuntimeError("hipcc failed: %s\n%s" % (" ".join(cmd), r.stdout))
         return obj
 
     if verbose:
-        print("hipcc %s -> %s (%d units, %s)" % (" ".join(base[1:]), out, len(units), objdir), flush=True)
-    try:
-        with concurrent.futures.ThreadPoolExecutor(jobs or _jobs()) as ex:
-            objs = list(ex.map(compile_one, units))
-        subprocess.check_call([HIPCC, "--offload-arch=%s" % ARCH, "-shared", "-o", out + ".tmp"] + objs)
-        os.replace(out + ".tmp", out)
-    finally:
-        shutil.rmtree(objdir, ignore_errors=True)
+        print("hipcc %s -> %s (%d units, src %s)" % (" ".join(base[1:]), out, len(units), digest[:16]), flush=True)
+    with concurrent.futures.ThreadPoolExecutor(jobs or _jobs()) as ex:
+        objs = list(ex.map(compile_one, units))
+    subprocess.check_call([HIPCC, "--offload-arch=%s" % ARCH, "-shared", "-o", out + ".tmp"] + objs, cwd=ROOT)
+    os.replace(out + ".tmp", out)
     return out
 
 

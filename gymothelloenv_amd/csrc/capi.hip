@@ -119,7 +119,12 @@ extern "C" {
 
 const char* oth_last_error(void) { return g_last_error.c_str(); }
 
-const char* oth_version(void) { return "othello_mi355x 0.1 (gfx950)"; }
+#ifndef OTH_SRC_HASH
+#define OTH_SRC_HASH "0000000000000000000000000000000000000000000000000000000000000000"
+#endif
+// build.py passes the SHA-256 of the sources and flags; the loader compares it
+// with the tree's sources (gymothelloenv_amd/build.py: embedded_hash)
+const char* oth_version(void) { return "othello_mi355x 0.2 (gfx950) oth-src-sha256:" OTH_SRC_HASH; }
 
 int oth_create(int32_t n_envs, int32_t board_size, uint32_t flags, uint64_t seed, uint32_t env_id_base,
                int32_t initial_rand_steps, int32_t device, oth_env** out) {

@@ -13,23 +13,28 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboth_oracle.so")
+BB_PATH = os.path.join(HERE, "libcpu_bitboard.so")
 
 F_SUDDEN_DEATH = 1
 F_DISK_REWARD = 2
 F_AUTO_RESET = 4
 
 _lib = None
+_bb = None
 
 
 def build():
     subprocess.check_call(["make", "-s", "-C", HERE])
 
 
+def _stale(out, *srcs):
+    return not os.path.exists(out) or any(os.path.getmtime(out) < os.path.getmtime(s) for s in srcs)
+
+
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH) or (os.path.getmtime(LIB_PATH) <
-                                            os.path.getmtime(os.path.join(HERE, "othello_oracle.c"))):
+        if _stale(LIB_PATH, os.path.join(HERE, "othello_oracle.c")):
             build()
         L = ctypes.CDLL(LIB_PATH)
         P = ctypes.c_void_p
@@ -49,6 +54,22 @@ def lib():
         L.oracle_step_vs.argtypes = [i32, u32, i32, i32, u64, u32, u64, i32, P, P, P, P, P, P, P, P, P]
         _lib = L
     return _lib
+
+
+def bb_lib():
+    """The bitboard CPU baseline (cpu_bitboard.cpp): bench.py's "best CPU" leg."""
+    global _bb
+    if _bb is None:
+        if _stale(BB_PATH, os.path.join(HERE, "cpu_bitboard.cpp"),
+                  os.path.join(HERE, "..", "gymothelloenv_amd", "csrc", "bitboard.hpp")):
+            build()
+        L = ctypes.CDLL(BB_PATH)
+        P = ctypes.c_void_p
+        L.cpu_bb_rollout.argtypes = [ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                                     ctypes.c_int32, ctypes.c_int32, P, P, P, P, P, P, P]
+        L.cpu_bb_rollout.restype = ctypes.c_int64
+        _bb = L
+    return _bb
 
 
 def _p(a):
@@ -121,6 +142,20 @@ def rollout(s, flags, policy, plies, seed=0, id_base=0, ply0=0, initial_rand_ste
     lib().oracle_rollout(s.n, flags, policy, initial_rand_steps, seed, id_base, ply0, E, plies,
                          _p(s.boards), _p(s.meta), _p(s.legal), _p(acts), _p(rews), _p(dns), _p(wdl))
     return acts, rews, dns, wdl
+
+
+def bb_rollout(s, plies, seed=0, id_base=0, ply0=0, record=True, wdl=None):
+    """Random-play rollout with the bitboard CPU baseline, in place (auto-reset,
+    sudden death irrelevant: random picks are legal).  Returns (actions,
+    rewards, dones or None, wdl, env-steps taken)."""
+    E = s.E
+    acts = np.zeros((plies, E), dtype=np.int32) if record else None
+    rews = np.zeros((plies, E), dtype=np.int32) if record else None
+    dns = np.zeros((plies, E), dtype=np.uint8) if record else None
+    wdl = np.zeros(3, dtype=np.int64) if wdl is None else wdl
+    steps = bb_lib().cpu_bb_rollout(s.n, seed, id_base, ply0, E, plies, _p(s.boards), _p(s.meta), _p(s.legal),
+                                    _p(acts), _p(rews), _p(dns), _p(wdl))
+    return acts, rews, dns, wdl, steps
 
 
 def greedy(s):

@@ -360,6 +360,7 @@ int oracle_step_batch(int n, uint32_t flags, uint64_t seed, uint32_t id_base, ui
  * index k = floor(u32 * len / 2^32) into the ascending possible_moves list;
  * u = word (ply % 4) of the Philox block with counter ply / 4. */
 static int random_action(const oenv *e, uint64_t seed, uint32_t id, uint64_t ply) {
+    if (e->nmoves == 0) return -1; /* no legal move: the invalid path, as on the device */
     uint32_t c[4] = {id, (uint32_t)(ply >> 2), (uint32_t)(ply >> 34), 0};
     philox((uint32_t)seed, (uint32_t)(seed >> 32), c);
     uint32_t u = c[ply & 3];

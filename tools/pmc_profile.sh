@@ -3,7 +3,7 @@
 # Usage: bash tools/pmc_profile.sh <outdir> [bench args...]
 set -e
 OUT=${1:-gpurun_out/pmc}; shift || true
-ARGS=${@:-"--steps 1000 --warmup 100 --no-cpu-baseline --no-single-ply --no-masked"}
+ARGS=${@:-"--steps 50 --warmup 5 --no-cpu-baseline --no-side"}
 mkdir -p $OUT
 export TMPDIR=/tmp
 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
