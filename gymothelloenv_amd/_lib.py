@@ -28,6 +28,9 @@ OTH_OBS_MAKE_STATE = 2
 OTH_OBS_ABSOLUTE = 3
 OTH_I8, OTH_I32, OTH_I64, OTH_F32, OTH_F64 = range(5)
 OTH_MASKED_SAMPLE, OTH_MASKED_MODE, OTH_MASKED_EVAL = range(3)
+OTH_MASKED_FULL_ENTROPY = 4
+OTH_GRAPH_SLOTS = 64
+OTH_GRAPH_COUNTER_SHIFT = 40
 
 # every symbol include/othello_mi355x.h declares: (restype, argtypes)
 _P = ctypes.c_void_p
@@ -54,8 +57,9 @@ SIGNATURES = {
     "oth_sample_actions": (_I32, [_P, _P, _I64, _P, _U64, _I32, _P, _P, _P, _P]),
     "oth_ply_counter": (_U64, [_P]),
     "oth_set_ply_counter": (_I32, [_P, _U64]),
-    "oth_graph_advance": (_I32, [_P, _U64, _U64, _P]),
-    "oth_counter_offsets": (_I32, [_P, _P]),
+    "oth_graph_begin": (_I32, [_P, _P]),
+    "oth_graph_end": (_I32, [_P, _U64, _I32, _P, _P]),
+    "oth_graph_offsets": (_I32, [_P, _I32, _P]),
     "oth_shape": (_I32, [_P, _P, _P, _P]),
     "oth_last_error": (ctypes.c_char_p, []),
     "oth_version": (ctypes.c_char_p, []),

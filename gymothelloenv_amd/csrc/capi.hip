@@ -156,8 +156,12 @@ int oth_create(int32_t n_envs, int32_t board_size, uint32_t flags, uint64_t seed
     const size_t slot_bytes = (size_t)env->nslots * 4 * sizeof(unsigned long long);
     if (err == hipSuccess) err = hipMalloc((void**)&env->wdl, slot_bytes);
     if (err == hipSuccess) err = hipMemset(env->wdl, 0, slot_bytes);
-    if (err == hipSuccess) err = hipMalloc((void**)&env->ctr_off, 2 * sizeof(uint64_t));
-    if (err == hipSuccess) err = hipMemset(env->ctr_off, 0, 2 * sizeof(uint64_t));
+    const size_t ctr_bytes = (size_t)OTH_GRAPH_SLOTS * 2 * sizeof(uint64_t);
+    if (err == hipSuccess) err = hipMalloc((void**)&env->ctr_slots, ctr_bytes);
+    if (err == hipSuccess) err = hipMemset(env->ctr_slots, 0, ctr_bytes);
+    env->cur_off = env->ctr_slots;
+    env->graph_slot = 0;
+    env->next_slot = 1;
     if (err != hipSuccess) {
         oth_destroy(env);
         return hip_fail(err, "oth_create: allocation");
@@ -182,7 +186,7 @@ int oth_destroy(oth_env* env) {
     if (env->meta) (void)hipFree(env->meta);
     if (env->legal) (void)hipFree(env->legal);
     if (env->wdl) (void)hipFree(env->wdl);
-    if (env->ctr_off) (void)hipFree(env->ctr_off);
+    if (env->ctr_slots) (void)hipFree(env->ctr_slots);
     delete env;
     return OTH_OK;
 }
@@ -278,7 +282,8 @@ int oth_masked_sample(int32_t board_size, int32_t n, const float* logits, int64_
                       int32_t* actions, float* log_probs, float* entropy, oth_stream_t stream) {
     const int bs = board_size < 4 ? 4 : board_size;
     if (bs > 16) return fail(OTH_EINVAL, "board_size must be <= 16");
-    if (mode < OTH_MASKED_SAMPLE || mode > OTH_MASKED_EVAL) return fail(OTH_EINVAL, "unknown mode");
+    if ((mode & ~OTH_MASKED_FULL_ENTROPY) < OTH_MASKED_SAMPLE || (mode & ~OTH_MASKED_FULL_ENTROPY) > OTH_MASKED_EVAL)
+        return fail(OTH_EINVAL, "unknown mode");
     if (n < 0 || (n > 0 && (!logits || !legal || !actions))) return fail(OTH_EINVAL, "bad arguments");
     if (ld < (int64_t)bs * bs) return fail(OTH_EINVAL, "ld < board_size^2");
     if (n == 0) return OTH_OK;
@@ -290,14 +295,15 @@ int oth_sample_actions(oth_env* env, const float* logits, int64_t ld, const floa
                        int32_t mode, int32_t* actions, float* log_probs, float* entropy, oth_stream_t stream) {
     OTH_CHECK_ENV(env);
     if (!logits || !actions) return fail(OTH_EINVAL, "logits / actions is NULL");
-    if (mode < OTH_MASKED_SAMPLE || mode > OTH_MASKED_EVAL) return fail(OTH_EINVAL, "unknown mode");
+    if ((mode & ~OTH_MASKED_FULL_ENTROPY) < OTH_MASKED_SAMPLE || (mode & ~OTH_MASKED_FULL_ENTROPY) > OTH_MASKED_EVAL)
+        return fail(OTH_EINVAL, "unknown mode");
     if (ld < (int64_t)env->n * env->n) return fail(OTH_EINVAL, "ld < N*N");
     return launch_masked(env->n, env->E, logits, (long long)ld, env->legal, uniforms, env->seed, env->id_base, counter,
-                         env->ctr_off + 1, mode, actions, log_probs, entropy, (hipStream_t)stream);
+                         env->cur_off + 1, mode, actions, log_probs, entropy, (hipStream_t)stream);
 }
 
-// The counters' device offsets move on by what one replay of a captured region
-// consumed (enqueued as the region's last node, so every replay advances them).
+// A graph region's offsets move on by what one replay consumed (enqueued as
+// the region's last node, so every replay advances them).
 __global__ void k_graph_advance(uint64_t* __restrict__ off, uint64_t d_ply, uint64_t d_sample) {
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         off[0] += d_ply;
@@ -305,18 +311,41 @@ __global__ void k_graph_advance(uint64_t* __restrict__ off, uint64_t d_ply, uint
     }
 }
 
-int oth_graph_advance(oth_env* env, uint64_t d_ply, uint64_t d_sample, oth_stream_t stream) {
-    OTH_CHECK_ENV(env);
-    hipLaunchKernelGGL(k_graph_advance, dim3(1), dim3(64), 0, (hipStream_t)stream, env->ctr_off, d_ply, d_sample);
-    return oth_host::after_launch("oth_graph_advance");
+int oth_graph_begin(oth_env* env, int32_t* slot) {
+    if (!env || !slot) return fail(OTH_EINVAL, "NULL argument");
+    if (env->graph_slot) return fail(OTH_EINVAL, "a graph region is already open on this handle");
+    if (env->next_slot >= OTH_GRAPH_SLOTS) return fail(OTH_EINVAL, "no graph counter slot left on this handle");
+    const int k = env->next_slot++;
+    env->graph_slot = k;
+    env->ply_saved = env->ply;
+    env->ply = (uint64_t)k << OTH_GRAPH_COUNTER_SHIFT;
+    env->cur_off = env->ctr_slots + 2 * k;
+    *slot = k;
+    return OTH_OK;
 }
 
-int oth_counter_offsets(const oth_env* env, uint64_t* out) {
+int oth_graph_end(oth_env* env, uint64_t d_sample, int32_t enqueue, uint64_t* d_ply, oth_stream_t stream) {
+    if (!env) return fail(OTH_EINVAL, "NULL oth_env");
+    if (!env->graph_slot) return fail(OTH_EINVAL, "no graph region is open on this handle");
+    const int k = env->graph_slot;
+    const uint64_t dp = env->ply - ((uint64_t)k << OTH_GRAPH_COUNTER_SHIFT);
+    env->ply = env->ply_saved;  // eager counting resumes where it was
+    env->cur_off = env->ctr_slots;
+    env->graph_slot = 0;
+    if (d_ply) *d_ply = dp;
+    if (!enqueue) return OTH_OK;
+    OTH_CHECK_ENV(env);
+    hipLaunchKernelGGL(k_graph_advance, dim3(1), dim3(64), 0, (hipStream_t)stream, env->ctr_slots + 2 * k, dp,
+                       d_sample);
+    return oth_host::after_launch("oth_graph_end");
+}
+
+int oth_graph_offsets(const oth_env* env, int32_t slot, uint64_t* out) {
     OTH_CHECK_ENV(env);
     if (!out) return fail(OTH_EINVAL, "out is NULL");
-    OTH_HIP(hipSetDevice(env->device));
+    if (slot < 0 || slot >= OTH_GRAPH_SLOTS) return fail(OTH_EINVAL, "slot out of range");
     OTH_HIP(hipDeviceSynchronize());
-    OTH_HIP(hipMemcpy(out, env->ctr_off, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    OTH_HIP(hipMemcpy(out, env->ctr_slots + 2 * slot, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return OTH_OK;
 }
 
@@ -383,11 +412,8 @@ uint64_t oth_ply_counter(const oth_env* env) { return env ? env->ply : 0; }
 
 int oth_set_ply_counter(oth_env* env, uint64_t ply) {
     if (!env) return fail(OTH_EINVAL, "NULL oth_env");
-    env->ply = ply;
-    // the counters are absolute again: drop what graph replays added
-    OTH_HIP(hipSetDevice(env->device));
-    OTH_HIP(hipDeviceSynchronize());
-    OTH_HIP(hipMemset(env->ctr_off, 0, 2 * sizeof(uint64_t)));
+    if (env->graph_slot) return fail(OTH_EINVAL, "cannot set the ply counter inside a graph region");
+    env->ply = ply;  // host only: graph regions keep their own counter ranges
     return OTH_OK;
 }
 

@@ -819,14 +819,14 @@ struct Rng {
     uint64_t seed;
     uint32_t id_base;
     int init_rand;
-    const uint64_t* ply_off;  // device offset of the ply counter: 0 eagerly, advanced by graph replays
+    const uint64_t* ply_off;  // device offset of the ply counter: slot 0 (= 0) eagerly, a graph region's slot under capture
 };
 
 template <int N>
 __global__ __launch_bounds__(BLOCK) void k_reset(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
                                                  uint64_t* __restrict__ legal, int E,
                                                  const uint8_t* __restrict__ mask, Rng rng, uint64_t ply) {
-    ply += *rng.ply_off;  // oth_graph_advance
+    ply += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
     const int e = blockIdx.x * BLOCK + threadIdx.x;
     if (e >= E) return;
     if (mask && !mask[e]) return;
@@ -842,7 +842,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(uint64_t* __restrict__ boards, u
                                                 const int32_t* __restrict__ actions, int32_t* __restrict__ rewards,
                                                 uint8_t* __restrict__ dones, unsigned long long* __restrict__ wdl,
                                                 Rng rng, uint64_t ply) {
-    ply += *rng.ply_off;  // oth_graph_advance
+    ply += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
     const int e = blockIdx.x * BLOCK + threadIdx.x;
     uint32_t cb = 0, cd = 0, cw = 0;
     if (e < E) {
@@ -876,7 +876,7 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
                                                 int32_t* __restrict__ actions, int32_t* __restrict__ rewards,
                                                 uint8_t* __restrict__ dones, unsigned long long* __restrict__ wdl,
                                                 Rng rng, uint64_t ply0) {
-    ply0 += *rng.ply_off;  // oth_graph_advance
+    ply0 += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
     __shared__ __attribute__((aligned(16))) uint64_t lds_rays[Eng::RAY_WORDS > 0 ? Eng::RAY_WORDS : 1];
     if constexpr (is_fills_w<Eng>::value) Eng::fill(lds_rays);
     else if constexpr (Eng::RAY_WORDS > 0) fill_rays<N>(lds_rays);
@@ -1036,7 +1036,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset_vs(uint64_t* __restrict__ board
                                                     uint64_t* __restrict__ legal, int E, uint32_t flags,
                                                     const int8_t* __restrict__ prot, const uint8_t* __restrict__ mask,
                                                     Rng rng, uint64_t call) {
-    call += *rng.ply_off;  // oth_graph_advance
+    call += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
     const int e = blockIdx.x * BLOCK + threadIdx.x;
     if (e >= E) return;
     if (mask && !mask[e]) return;
@@ -1054,7 +1054,7 @@ __global__ __launch_bounds__(BLOCK) void k_step_vs(uint64_t* __restrict__ boards
                                                    int32_t* __restrict__ rewards, uint8_t* __restrict__ dones,
                                                    int32_t* __restrict__ plies_out,
                                                    unsigned long long* __restrict__ wdl, Rng rng, uint64_t call) {
-    call += *rng.ply_off;  // oth_graph_advance
+    call += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
     const int e = blockIdx.x * BLOCK + threadIdx.x;
     uint32_t cb = 0, cd = 0, cw = 0;
     if (e < E) {

@@ -17,7 +17,7 @@ namespace {
 
 int grid_for(long long work) { return (int)((work + BLOCK - 1) / BLOCK); }
 
-Rng rng_of(const oth_env* env) { return Rng{env->seed, env->id_base, env->init_rand, env->ctr_off}; }
+Rng rng_of(const oth_env* env) { return Rng{env->seed, env->id_base, env->init_rand, env->cur_off}; }
 
 // Compile-time policy for a runtime id (OTH_POLICY_*); MAXIMIN1 is GREEDY
 // (same move: simple_policies.py:111-155 at depth 1 is GreedyPolicy's argmax).

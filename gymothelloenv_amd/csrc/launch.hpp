@@ -22,7 +22,16 @@ struct oth_env {
     uint64_t* legal;
     unsigned long long* wdl;  // [nslots][4] per-block W/D/L slots (tally)
     int32_t nslots;
-    uint64_t* ctr_off;  // device [2]: offsets added to the ply counter / the sample counter (graph replays)
+    // Philox counter offsets (HIP-graph regions, oth_graph_begin/_end):
+    // device [OTH_GRAPH_SLOTS][2] = (ply, sample) offsets; slot 0 serves eager
+    // launches and stays 0, slot k > 0 belongs to graph region k, whose
+    // captured counters start at k << OTH_GRAPH_COUNTER_SHIFT and whose offset
+    // moves on by what one replay consumed.
+    uint64_t* ctr_slots;
+    const uint64_t* cur_off;  // the slot launches read now (slot 0 outside a region)
+    int32_t graph_slot;       // open region (0: none)
+    int32_t next_slot;        // next free slot
+    uint64_t ply_saved;       // eager ply counter while a region is open
 };
 
 namespace oth_host {

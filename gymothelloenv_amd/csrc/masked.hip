@@ -141,7 +141,7 @@ __device__ __forceinline__ void load_slot(Slot<CH, G>& b, int l, int NN, const f
     }
 }
 
-template <int CH, int G>
+template <int CH, int G, bool FULL>
 __device__ __forceinline__ void finish_slot(Slot<CH, G>& b, int l, int NN, const float* __restrict__ logits,
                                             long long ld, const float* __restrict__ uniforms, uint64_t seed,
                                             uint32_t id_base, uint64_t counter, int mode,
@@ -149,6 +149,32 @@ __device__ __forceinline__ void finish_slot(Slot<CH, G>& b, int l, int NN, const
                                             float* __restrict__ entropy) {
     constexpr int NB = Slot<CH, G>::NB;
     const int e = b.e;
+    // OTH_MASKED_FULL_ENTROPY: entropy of the unmasked categorical over all N*N
+    // squares (Policy.evaluate_actions' dist.entropy(), model.py:175)
+    float full_ent = 0.f;
+    if constexpr (FULL) {
+        float fm = -INFINITY;
+#pragma unroll
+        for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (4 * G * bi + 4 * l + j < NN) fm = fmaxf(fm, b.x[bi][j]);
+        fm = Grp<G>::max(fm);
+        float fs = 0.f, fsx = 0.f;
+#pragma unroll
+        for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (4 * G * bi + 4 * l + j < NN) {
+                    const float d = b.x[bi][j] - fm;
+                    const float q = __expf(d);
+                    fs += q;
+                    fsx = fmaf(q, d, fsx);
+                }
+        fs = Grp<G>::sum(fs);
+        fsx = Grp<G>::sum(fsx);
+        full_ent = __logf(fs) - fsx / fs;
+    }
     // illegal squares -> -inf: they drop out of the max and get p = exp(-inf) = 0
     float m = -INFINITY;
 #pragma unroll
@@ -232,12 +258,12 @@ __device__ __forceinline__ void finish_slot(Slot<CH, G>& b, int l, int NN, const
             if (a >= 64 * c && a < 64 * c + 64 && a < NN) choice = (b.words[c] >> (a - 64 * c)) & 1ull;
         if (mode != OTH_MASKED_EVAL) actions[e] = a;
         if (log_probs) log_probs[e] = choice ? logits[(size_t)e * (size_t)ld + a] - m - logS : 0.f;
-        if (entropy) entropy[e] = any ? logS - SX / tot : 0.f;
+        if (entropy) entropy[e] = FULL ? full_ent : (any ? logS - SX / tot : 0.f);
     }
 }
 
 // BPR boards per lane group: group r of the grid owns boards r*BPR .. r*BPR + BPR - 1.
-template <int CH, int G, bool VEC, int BPR>
+template <int CH, int G, bool VEC, int BPR, bool FULL>
 __global__ __launch_bounds__(MS_BLOCK) void k_masked(int E, int NN, const float* __restrict__ logits, long long ld,
                                                      const uint64_t* __restrict__ legal,
                                                      const float* __restrict__ uniforms, uint64_t seed,
@@ -245,7 +271,7 @@ __global__ __launch_bounds__(MS_BLOCK) void k_masked(int E, int NN, const float*
                                                      const uint64_t* __restrict__ counter_off, int mode,
                                                      int32_t* __restrict__ actions, float* __restrict__ log_probs,
                                                      float* __restrict__ entropy) {
-    if (counter_off) counter += *counter_off;  // graph replays advance the device offset (oth_graph_advance)
+    if (counter_off) counter += *counter_off;  // graph-region offset (oth_graph_end); 0 eagerly
     const long long t = (long long)blockIdx.x * MS_BLOCK + threadIdx.x;
     const int l = (int)(t % G);
     Slot<CH, G> b[BPR];
@@ -258,22 +284,35 @@ __global__ __launch_bounds__(MS_BLOCK) void k_masked(int E, int NN, const float*
     }
 #pragma unroll
     for (int k = 0; k < BPR; ++k)
-        finish_slot<CH, G>(b[k], l, NN, logits, ld, uniforms, seed, id_base, counter, mode, actions, log_probs,
+        finish_slot<CH, G, FULL>(b[k], l, NN, logits, ld, uniforms, seed, id_base, counter, mode, actions, log_probs,
                            entropy);
+}
+
+template <int CH, int G, int BPR, bool FULL>
+void launch_one(bool vec, int E, hipStream_t st, int NN, const float* logits, long long ld, const uint64_t* legal,
+               const float* uniforms, uint64_t seed, uint32_t id_base, uint64_t counter, const uint64_t* counter_off,
+               int mode, int32_t* actions, float* log_probs, float* entropy) {
+    const long long groups = ((long long)E + BPR - 1) / BPR;
+    const int grid = (int)((groups * G + MS_BLOCK - 1) / MS_BLOCK);
+    if (vec)
+        hipLaunchKernelGGL((k_masked<CH, G, true, BPR, FULL>), dim3(grid), dim3(MS_BLOCK), 0, st, E, NN, logits, ld,
+                           legal, uniforms, seed, id_base, counter, counter_off, mode, actions, log_probs, entropy);
+    else
+        hipLaunchKernelGGL((k_masked<CH, G, false, BPR, FULL>), dim3(grid), dim3(MS_BLOCK), 0, st, E, NN, logits, ld,
+                           legal, uniforms, seed, id_base, counter, counter_off, mode, actions, log_probs, entropy);
 }
 
 template <int CH, int G, int BPR>
 void launch_ch(bool vec, int E, hipStream_t st, int NN, const float* logits, long long ld, const uint64_t* legal,
                const float* uniforms, uint64_t seed, uint32_t id_base, uint64_t counter, const uint64_t* counter_off,
                int mode, int32_t* actions, float* log_probs, float* entropy) {
-    const long long groups = ((long long)E + BPR - 1) / BPR;
-    const int grid = (int)((groups * G + MS_BLOCK - 1) / MS_BLOCK);
-    if (vec)
-        hipLaunchKernelGGL((k_masked<CH, G, true, BPR>), dim3(grid), dim3(MS_BLOCK), 0, st, E, NN, logits, ld,
-                           legal, uniforms, seed, id_base, counter, counter_off, mode, actions, log_probs, entropy);
+    const int base = mode & 3;
+    if (mode & OTH_MASKED_FULL_ENTROPY)
+        launch_one<CH, G, BPR, true>(vec, E, st, NN, logits, ld, legal, uniforms, seed, id_base, counter, counter_off,
+                                     base, actions, log_probs, entropy);
     else
-        hipLaunchKernelGGL((k_masked<CH, G, false, BPR>), dim3(grid), dim3(MS_BLOCK), 0, st, E, NN, logits, ld,
-                           legal, uniforms, seed, id_base, counter, counter_off, mode, actions, log_probs, entropy);
+        launch_one<CH, G, BPR, false>(vec, E, st, NN, logits, ld, legal, uniforms, seed, id_base, counter,
+                                      counter_off, base, actions, log_probs, entropy);
 }
 
 }  // namespace

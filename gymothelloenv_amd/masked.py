@@ -78,10 +78,13 @@ def masked_sample(logits, legal, board_size, mode="sample", uniforms=None, seed=
     return acts, lp, ent
 
 
-def masked_log_prob(logits, legal, actions, board_size, entropy=True):
+def masked_log_prob(logits, legal, actions, board_size, entropy=True, full_entropy=False):
     """evaluate_actions: log-prob of `actions` (n,) among each row's legal
     squares (0 where the row has none or the action is not one of them) and
-    the masked entropy.  Returns (log_probs float32, entropy float32 or None)."""
+    the entropy per row: of the masked distribution, or with full_entropy=True
+    of the unmasked categorical over all squares, which is what
+    Policy.evaluate_actions reports (model.py:175, dist.entropy(); it returns
+    the mean).  Returns (log_probs float32, entropy float32 or None)."""
     lib = L.load()
     bs = max(4, int(board_size))
     x = _rows(logits, bs)
@@ -91,6 +94,7 @@ def masked_log_prob(logits, legal, actions, board_size, entropy=True):
     lp = torch.empty(n, dtype=torch.float32, device=x.device)
     ent = torch.empty(n, dtype=torch.float32, device=x.device) if entropy else None
     stream = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
-    L.check(lib.oth_masked_sample(bs, n, _ptr(x), x.stride(0), _ptr(legal), None, 0, 0, 0, L.OTH_MASKED_EVAL,
+    mode = L.OTH_MASKED_EVAL | (L.OTH_MASKED_FULL_ENTROPY if full_entropy else 0)
+    L.check(lib.oth_masked_sample(bs, n, _ptr(x), x.stride(0), _ptr(legal), None, 0, 0, 0, mode,
                                   _ptr(acts), _ptr(lp), _ptr(ent), stream), "oth_masked_sample")
     return lp, ent

@@ -71,6 +71,7 @@ class VecOthelloEnv(object):
                                          ctypes.byref(h)), "oth_create")
         self._h = h
         self._sample_calls = 0  # Philox counter of sample_actions
+        self._region_resets = None  # resets inside an open graph region (None: no region)
 
     # ------------------------------------------------------------------ utils
     def _stream(self):
@@ -99,6 +100,8 @@ class VecOthelloEnv(object):
 
     @ply_counter.setter
     def ply_counter(self, v):
+        if getattr(self, "_region_resets", None) is not None:
+            raise RuntimeError("cannot set the ply counter inside a graph region")
         L.check(self._lib.oth_set_ply_counter(self._h, int(v)), "oth_set_ply_counter")
 
     # ---------------------------------------------------------------- the API
@@ -107,6 +110,8 @@ class VecOthelloEnv(object):
         m = None
         if mask is not None:
             m = mask.to(device=self.device, dtype=torch.uint8).contiguous()
+        if getattr(self, "_region_resets", None) is not None:
+            self._region_resets += 1
         L.check(self._lib.oth_reset(self._h, _ptr(m), self._stream()), "oth_reset")
         return self.get_observation()
 
@@ -279,39 +284,83 @@ class VecOthelloEnv(object):
         self._sample_calls += 1
         return acts, lp, ent
 
-    def counter_offsets(self):
-        """Device offsets graph replays added to (ply counter, sample counter); synchronises."""
+    @property
+    def sample_counter(self):
+        """Philox counter of the next eager sample_actions call (purpose 3)."""
+        return self._sample_calls
+
+    @sample_counter.setter
+    def sample_counter(self, v):
+        self._sample_calls = int(v)
+
+    @staticmethod
+    def graph_counter_base(slot):
+        """First counter of graph region `slot`'s range (ply and sample counters)."""
+        return int(slot) << L.OTH_GRAPH_COUNTER_SHIFT
+
+    def graph_offsets(self, slot):
+        """(ply, sample) offsets graph region `slot`'s replays have consumed;
+        synchronises the device, so never call it during a capture."""
+        _no_capture("graph_offsets")
         out = (ctypes.c_uint64 * 2)()
-        L.check(self._lib.oth_counter_offsets(self._h, out), "oth_counter_offsets")
+        L.check(self._lib.oth_graph_offsets(self._h, int(slot), out), "oth_graph_offsets")
         return int(out[0]), int(out[1])
 
     @contextlib.contextmanager
     def graph_region(self):
-        """Wrap the calls captured into a HIP graph (inside `torch.cuda.graph`):
-        on exit it enqueues oth_graph_advance with what the region consumed of the
-        ply and sample counters, so every replay draws fresh Philox numbers
-        (random openings, the device opponents, sample_actions without uniforms)
-        instead of the capture-time ones.  Outside a capture it enqueues nothing
-        (the host counters already moved on).
+        """Wrap the calls captured into a HIP graph (enter it INSIDE
+        `torch.cuda.graph`).  The region owns a counter range of its own
+        (oth_graph_begin: ply and sample counters from slot << 40), and on exit
+        enqueues the advance of its device offsets by what the region consumed,
+        so replay r draws counters base + r*d .. base + r*d + d - 1: fresh
+        Philox numbers every replay (random openings, device opponents,
+        sample_actions without uniforms), disjoint from eager calls and from
+        every other region of this handle.  Yields the slot.
 
-            with torch.cuda.graph(g), env.graph_region():
+            with torch.cuda.graph(g), env.graph_region() as slot:
                 for k in range(K): env.step(env.sample_actions(actor(obs))[0]); ...
         """
-        ply0, smp0 = self.ply_counter, self._sample_calls
-        yield self
         if not torch.cuda.is_current_stream_capturing():
-            return
-        d_ply, d_smp = self.ply_counter - ply0, self._sample_calls - smp0
-        L.check(self._lib.oth_graph_advance(self._h, d_ply, d_smp, self._stream()), "oth_graph_advance")
+            raise RuntimeError("graph_region must be entered inside torch.cuda.graph(...) "
+                               "(with torch.cuda.graph(g), env.graph_region(): ...)")
+        slot = ctypes.c_int32()
+        L.check(self._lib.oth_graph_begin(self._h, ctypes.byref(slot)), "oth_graph_begin")
+        k = int(slot.value)
+        smp0, self._sample_calls = self._sample_calls, self.graph_counter_base(k)
+        self._region_resets = 0
+        ok = False
+        try:
+            yield k
+            ok = True
+        finally:
+            capturing = torch.cuda.is_current_stream_capturing()
+            d_smp = self._sample_calls - self.graph_counter_base(k)
+            self._sample_calls = smp0
+            d_ply = ctypes.c_uint64()
+            rc = self._lib.oth_graph_end(self._h, d_smp, int(capturing), ctypes.byref(d_ply), self._stream())
+            resets, self._region_resets = self._region_resets, None
+            if ok:
+                L.check(rc, "oth_graph_end")
+                if not capturing:
+                    raise RuntimeError("the capture ended inside graph_region: enter graph_region inside "
+                                       "torch.cuda.graph(...), not around it")
+                if resets and self.initial_rand_steps > 0 and d_ply.value == 0:
+                    raise RuntimeError("this graph region only resets boards with random openings: every replay "
+                                       "would draw the same openings; capture at least one ply with the reset")
 
     def state_dict(self):
+        """Boards, meta, possible_moves and the eager counters (host values).
+        Graph regions keep their own counter ranges and are not part of it."""
+        _no_capture("state_dict")
         b, m, lg = self.get_state()
-        off_ply, off_smp = self.counter_offsets()  # absolute counters, graph replays included
-        return {"boards": b, "meta": m, "legal": lg, "ply_counter": self.ply_counter + off_ply,
-                "sample_calls": self._sample_calls + off_smp, "board_size": self.board_size,
+        return {"boards": b, "meta": m, "legal": lg, "ply_counter": self.ply_counter,
+                "sample_calls": self._sample_calls, "board_size": self.board_size,
                 "num_envs": self.num_envs}
 
     def load_state_dict(self, sd):
+        """Restore a state_dict.  Graphs captured on this handle stay valid and
+        keep drawing from their own counter ranges (nothing is zeroed)."""
+        _no_capture("load_state_dict")
         if sd["board_size"] != self.board_size or sd["num_envs"] != self.num_envs:
             raise ValueError("state_dict shape does not match this env")
         self.set_state(sd["boards"], sd["meta"], sd["legal"])
@@ -331,6 +380,11 @@ class VecOthelloEnv(object):
         _, m, _ = self.get_state()
         w = (m >> 2) & 3
         return torch.where(w == 1, WHITE_DISK, torch.where(w == 2, BLACK_DISK, NO_DISK))
+
+
+def _no_capture(what):
+    if torch.cuda.is_current_stream_capturing():
+        raise RuntimeError("%s synchronises the device and cannot run during a HIP-graph capture" % what)
 
 
 def legal_moves(board_size, mover, opponent):

@@ -78,7 +78,11 @@ enum { OTH_I8 = 0, OTH_I32 = 1, OTH_I64 = 2, OTH_F32 = 3, OTH_F64 = 4 };
 enum {
     OTH_MASKED_SAMPLE = 0, /* FixedCategorical(...).sample() / np.random.choice: actions out */
     OTH_MASKED_MODE = 1,   /* FixedCategorical(...).mode(): first largest legal logit; actions out */
-    OTH_MASKED_EVAL = 2    /* evaluate_actions: actions in, log-probs of those actions out */
+    OTH_MASKED_EVAL = 2,   /* evaluate_actions: actions in, log-probs of those actions out */
+    /* or-ed into a mode: entropy[e] = entropy of the UNMASKED categorical over
+     * all N*N squares, as Policy.evaluate_actions returns it (dist.entropy(),
+     * model.py:175; the caller takes the mean) instead of the masked one */
+    OTH_MASKED_FULL_ENTROPY = 4
 };
 
 /* OthelloBaseEnv.__init__ (othello.py:222-254) for n_envs boards of size
@@ -195,20 +199,34 @@ int oth_masked_sample(int32_t board_size, int32_t n, const float *logits, int64_
 int oth_sample_actions(oth_env *env, const float *logits, int64_t ld, const float *uniforms, uint64_t counter,
                        int32_t mode, int32_t *actions, float *log_probs, float *entropy, oth_stream_t stream);
 
-/* Global ply counter of the handle (the Philox counter of the next ply; host
- * part, without the graph offset below).  Setting it also zeroes the offsets. */
+/* Global ply counter of the handle: the Philox counter of the next eager ply
+ * (random policy, openings, device opponents).  Host value only; setting it
+ * does not touch graph regions' counter ranges (below). */
 uint64_t oth_ply_counter(const oth_env *env);
 int oth_set_ply_counter(oth_env *env, uint64_t ply);
 
-/* HIP-graph support (no reference counterpart: the reference has no device).
+/* HIP-graph regions (no reference counterpart: the reference has no device).
  * Every entry point only enqueues kernels on `stream`, so a region of calls can
- * be captured and replayed; the Philox counters a capture bakes in (the ply
- * counter, the sample counter) are offset on the device by out[0] / out[1],
- * which oth_graph_advance -- enqueued as the region's last call -- moves on by
- * what one pass of the region consumed, so every replay draws fresh numbers.
- * Eagerly the offsets stay 0.  oth_counter_offsets synchronises the device. */
-int oth_graph_advance(oth_env *env, uint64_t d_ply, uint64_t d_sample, oth_stream_t stream);
-int oth_counter_offsets(const oth_env *env, uint64_t out[2]);
+ * be captured and replayed.  The Philox counters a capture bakes in are host
+ * values; to make every replay draw fresh numbers without reusing any counter
+ * of eager calls or of other graphs, each region owns a disjoint counter range:
+ *   oth_graph_begin: opens region k (k = 1 .. OTH_GRAPH_SLOTS-1, *slot = k);
+ *     until oth_graph_end the handle's ply counter runs from
+ *     k << OTH_GRAPH_COUNTER_SHIFT and launches add the device offsets of slot k;
+ *   oth_graph_end: closes it, restores the eager ply counter, *d_ply = plies
+ *     the region consumed; if enqueue != 0 it enqueues (as the region's last
+ *     node) the advance of slot k's offsets by (d_ply, d_sample), so replay r
+ *     draws the counters (k << SHIFT) + r * d + j.  d_sample is what the caller's
+ *     sample counter (oth_sample_actions) consumed inside the region, whose
+ *     range must start at k << SHIFT as well.
+ *   oth_graph_offsets: slot k's (ply, sample) offsets; synchronises the device
+ *     (never call it while a capture is active).
+ * Eager launches use slot 0, always 0. */
+#define OTH_GRAPH_SLOTS 64
+#define OTH_GRAPH_COUNTER_SHIFT 40
+int oth_graph_begin(oth_env *env, int32_t *slot);
+int oth_graph_end(oth_env *env, uint64_t d_sample, int32_t enqueue, uint64_t *d_ply, oth_stream_t stream);
+int oth_graph_offsets(const oth_env *env, int32_t slot, uint64_t out[2]);
 
 /* Handle geometry: n_envs, board_size, W. */
 int oth_shape(const oth_env *env, int32_t *n_envs, int32_t *board_size, int32_t *words);

@@ -144,6 +144,35 @@ def rollout(s, flags, policy, plies, seed=0, id_base=0, ply0=0, initial_rand_ste
     return acts, rews, dns, wdl
 
 
+def rollout_parallel(s, flags, policy, plies, seed=0, id_base=0, ply0=0, initial_rand_steps=0, threads=None):
+    """rollout() over contiguous board ranges on host threads (the ctypes call
+    releases the GIL); boards are independent and keyed by global id, so the
+    result equals one rollout() call.  For full-size replays (65,536 boards)."""
+    import concurrent.futures
+    E = s.E
+    T = max(1, min(threads or len(os.sched_getaffinity(0)), 16, E))
+    cuts = [E * k // T for k in range(T + 1)]
+    acts = np.zeros((plies, E), dtype=np.int32)
+    rews = np.zeros((plies, E), dtype=np.int32)
+    dns = np.zeros((plies, E), dtype=np.uint8)
+    wdls = np.zeros((T, 3), dtype=np.int64)
+
+    def part(k):
+        lo, hi = cuts[k], cuts[k + 1]
+        sub = State(s.n, hi - lo)
+        sub.boards[:] = s.boards[lo:hi]
+        sub.meta[:] = s.meta[lo:hi]
+        sub.legal[:] = s.legal[lo:hi]
+        a, r, d, w = rollout(sub, flags, policy, plies, seed=seed, id_base=id_base + lo, ply0=ply0,
+                             initial_rand_steps=initial_rand_steps)
+        acts[:, lo:hi], rews[:, lo:hi], dns[:, lo:hi], wdls[k] = a, r, d, w
+        s.boards[lo:hi], s.meta[lo:hi], s.legal[lo:hi] = sub.boards, sub.meta, sub.legal
+
+    with concurrent.futures.ThreadPoolExecutor(T) as ex:
+        list(ex.map(part, range(T)))
+    return acts, rews, dns, wdls.sum(0)
+
+
 def bb_rollout(s, plies, seed=0, id_base=0, ply0=0, record=True, wdl=None):
     """Random-play rollout with the bitboard CPU baseline, in place (auto-reset,
     sudden death irrelevant: random picks are legal).  Returns (actions,

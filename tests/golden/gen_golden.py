@@ -12,6 +12,7 @@ Bit convention used in every fixture: square a = row * N + col
 colour.
 
     python tests/golden/gen_golden.py        # rewrites tests/golden/*.npz|json
+    python tests/golden/gen_golden.py masked # only masked.npz (learners' policy heads)
 """
 import contextlib
 import io
@@ -418,11 +419,140 @@ def gen_maximin(othello, simple_policies):
     np.savez_compressed(os.path.join(OUT, "maximin.npz"), **out)
 
 
+def install_learner_shims():
+    """Stand-ins for what the learners' modules import but the policy heads never
+    use: torch.utils.tensorboard (ppo.py:7; tensorboard is absent), the
+    un-vendored `baselines` behind a2c_ppo_acktr/envs.py (utils.py:7 imports only
+    the VecNormalize name).  The `ppo` stub util.py needed is dropped so the real
+    ppo.py is imported."""
+    tb = types.ModuleType("torch.utils.tensorboard")
+    tb.SummaryWriter = object
+    envs = types.ModuleType("pytorch_a2c_ppo_acktr_gail.a2c_ppo_acktr.envs")
+    envs.VecNormalize = type("VecNormalize", (object,), {})
+    sys.modules.update({"torch.utils.tensorboard": tb, "pytorch_a2c_ppo_acktr_gail.a2c_ppo_acktr.envs": envs})
+    sys.modules.pop("ppo", None)
+
+
+def gen_masked(othello):
+    """The learners' masked policy heads on fixed logits, computed by the
+    reference's own code:
+      * Policy.act (model.py:60-99) with deterministic=True (mode) and False
+        (torch-seeded sample), actions and log-probs, through a Policy whose
+        base returns the fixture logits as actor features and whose
+        distributions.Categorical head has an identity linear layer;
+      * Policy.evaluate_actions (model.py:156-178): per-row log-probs of given
+        actions (legal, illegal and out of range) and dist_entropy (one row
+        per call, so the returned mean is the row's entropy);
+      * PPO.get_action (ppo.py:228-262): the renormalised probabilities over
+        possible_moves and np.random.choice's draw, with the uniform u that
+        numpy's legacy stream supplies to it (np.random.seed(k) then one
+        random_sample()).
+    Positions (possible_moves) come from reference random games; rows with no
+    legal move, exactly one, and tied logits are included."""
+    import torch
+    import torch.nn as nn
+    install_learner_shims()
+    from pytorch_a2c_ppo_acktr_gail.a2c_ppo_acktr import model as M  # noqa: E402  (reference)
+    from pytorch_a2c_ppo_acktr_gail.a2c_ppo_acktr.distributions import Categorical as RefCategorical  # noqa: E402
+    import ppo as P  # noqa: E402  (reference)
+
+    class Features(nn.Module):  # base(inputs, rnn_hxs, masks) -> (value, actor_features, rnn_hxs)
+        def forward(self, inputs, rnn_hxs, masks):
+            return torch.zeros(inputs.shape[0], 1), inputs, rnn_hxs
+
+    out = {}
+    for n in (6, 8):
+        nn_sq = n * n
+        rnd = np.random.RandomState(300 + n)
+        env = othello.OthelloBaseEnv(board_size=n, mute=True)
+        moves = []
+        while len(moves) < 1500:
+            env.reset()
+            done = False
+            while not done:
+                moves.append(list(env.possible_moves))
+                pm = env.possible_moves
+                _, _, done, _ = env.step(int(pm[rnd.randint(0, len(pm))]))
+        moves = moves[:1500] + [[] for _ in range(24)]  # + rows with no legal move
+        R = len(moves)
+        logits = (rnd.standard_normal((R, nn_sq)) * 3).astype(np.float32)
+        logits[::17] = 1.25  # ties: the mode is the lowest legal square
+        pol = M.Policy.__new__(M.Policy)
+        nn.Module.__init__(pol)
+        pol.base = Features()
+        pol.dist = RefCategorical(nn_sq, nn_sq)
+        with torch.no_grad():
+            pol.dist.linear.weight.copy_(torch.eye(nn_sq))
+            pol.dist.linear.bias.zero_()
+        pol.i, pol.e = 1, 1
+        x = torch.from_numpy(logits)
+        with torch.no_grad(), contextlib.redirect_stdout(io.StringIO()):
+            _, mode_a, mode_lp, _ = pol.act(x, None, None, moves, deterministic=True)
+            torch.manual_seed(n)
+            _, samp_a, samp_lp, _ = pol.act(x, None, None, moves, deterministic=False)
+            eval_a = samp_a.clone()
+            k = np.arange(R)
+            eval_a[k % 5 == 1, 0] = torch.from_numpy(rnd.randint(-3, nn_sq + 3, size=int((k % 5 == 1).sum())))
+            eval_lp, full_ent = [], []
+            for i in range(R):
+                _, lp, ent, _ = pol.evaluate_actions(x[i:i + 1], None, None, eval_a[i:i + 1], [moves[i]])
+                eval_lp.append(float(lp.reshape(-1)[0]))
+                full_ent.append(float(ent))
+        # PPO.get_action: renormalised probabilities + np.random.choice
+        agent = P.PPO.__new__(P.PPO)
+        agent.env = types.SimpleNamespace(possible_moves=None)
+
+        class Probs(object):
+            def get_action_probs(self, state):
+                return torch.softmax(state, dim=1)  # ActorCritic.action_and_value's softmax (ppo.py:73)
+
+        agent.policy_old = Probs()
+        seen = {}
+        real_choice = np.random.choice
+
+        def spy(a, p=None, **kw):
+            seen["p"] = np.array(p, dtype=np.float64)
+            return real_choice(a, p=p, **kw)
+
+        ppo_u, ppo_a, ppo_p = np.zeros(R), np.full(R, -1, dtype=np.int32), np.zeros((R, nn_sq))
+        np.random.choice = spy
+        try:
+            for i in range(R):
+                if not moves[i]:
+                    continue  # np.random.choice([]) fails in the reference (no legal move)
+                agent.env.possible_moves = moves[i]
+                np.random.seed(10000 + i)
+                ppo_u[i] = np.random.random_sample()
+                np.random.seed(10000 + i)
+                ppo_a[i] = agent.get_action(logits[i])
+                ppo_p[i, moves[i]] = seen["p"]
+        finally:
+            np.random.choice = real_choice
+        legal = np.array([pack_moves(m, n) for m in moves], dtype=np.uint64)
+        key = "N%d_" % n
+        out.update({key + "logits": logits, key + "legal": legal,
+                    key + "nlegal": np.array([len(m) for m in moves], dtype=np.int32),
+                    key + "mode_action": mode_a.numpy().reshape(-1).astype(np.int32),
+                    key + "mode_logp": np.asarray(mode_lp, dtype=np.float32).reshape(-1),
+                    key + "sample_action": samp_a.numpy().reshape(-1).astype(np.int32),
+                    key + "sample_logp": np.asarray(samp_lp, dtype=np.float32).reshape(-1),
+                    key + "eval_action": eval_a.numpy().reshape(-1).astype(np.int32),
+                    key + "eval_logp": np.array(eval_lp, dtype=np.float32),
+                    key + "full_entropy": np.array(full_ent, dtype=np.float32),
+                    key + "ppo_u": ppo_u, key + "ppo_action": ppo_a, key + "ppo_probs": ppo_p})
+        print("masked N=%d: %d rows (%d without a legal move, %d with one)" %
+              (n, R, sum(1 for m in moves if not m), sum(1 for m in moves if len(m) == 1)))
+    np.savez_compressed(os.path.join(OUT, "masked.npz"), **out)
+
+
 def main():
     install_shims()
     import othello  # noqa: E402  (reference, read-only)
     import simple_policies  # noqa: E402
     import util  # noqa: E402
+    if sys.argv[1:] == ["masked"]:
+        gen_masked(othello)
+        return
     gen_kat(othello)
     gen_trajectories(othello)
     gen_greedy(othello, simple_policies, util)
@@ -430,6 +560,7 @@ def main():
     gen_wrappers(othello, simple_policies)
     gen_vs(othello)
     gen_maximin(othello, simple_policies)
+    gen_masked(othello)
 
 
 if __name__ == "__main__":

@@ -45,3 +45,16 @@ def test_oracle_random_action_without_moves_is_invalid():
     a, r, d, _ = oracle.rollout(s, oracle.F_SUDDEN_DEATH, 0, 1, seed=0)
     assert (a[0] == -1).all()
     assert (d[0] == 1).all() and (r[0] == -1).all()  # sudden death: the mover loses
+
+
+def test_threaded_oracle_rollout_equals_single_call():
+    """oracle.rollout_parallel (the full-size GPU replays' checker) == rollout()."""
+    s1 = oracle.reset_openings(8, 999, 4, 0, 0, 6)
+    s2 = s1.copy()
+    r1 = oracle.rollout(s1, 5, 1, 50, seed=4, initial_rand_steps=6)
+    r2 = oracle.rollout_parallel(s2, 5, 1, 50, seed=4, initial_rand_steps=6, threads=5)
+    for x, y in zip(r1, r2):
+        np.testing.assert_array_equal(x, y)
+    np.testing.assert_array_equal(s1.boards, s2.boards)
+    np.testing.assert_array_equal(s1.meta, s2.meta)
+    np.testing.assert_array_equal(s1.legal, s2.legal)

@@ -6,7 +6,8 @@ dones, W/D/L) -- the launch-bound single-ply path of ppo.py-style training
 
 Plain capture needs caller-supplied uniforms and initial_rand_steps = 0 (the
 Philox counters are host values frozen at capture); VecOthelloEnv.graph_region
-lifts that by advancing device offsets of both counters once per replay."""
+lifts that: the region gets a counter range of its own and a device offset
+that moves on by what one replay consumed."""
 import numpy as np
 import pytest
 
@@ -64,12 +65,17 @@ def test_graph_replay_equals_eager(torch_gpu, n):
     assert int(eager.counts().sum()) > 0
 
 
+def _set_counters(env, c):
+    env.ply_counter = c
+    env.sample_counter = c
+
+
 @pytest.mark.parametrize("n", [6, 8])
 def test_graph_region_fresh_draws(torch_gpu, n):
     """graph_region: device-drawn samples (no uniforms) and random openings
-    (initial_rand_steps > 0) under replay advance the Philox counters on the
-    device, so replay r equals eager plies r*K .. r*K+K-1 of a twin env and two
-    replays draw different actions."""
+    (initial_rand_steps > 0) under replay draw from the region's own counter
+    range: replay r equals eager plies at counters base + r*K .. of a twin
+    env, and two replays draw different actions."""
     torch = torch_gpu
     from gymothelloenv_amd import VecOthelloEnv
     E, K = 2048, 8
@@ -89,15 +95,17 @@ def test_graph_region_fresh_draws(torch_gpu, n):
         out[k].copy_(act)
 
     graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph), graphed.graph_region():
+    with torch.cuda.graph(graph), graphed.graph_region() as slot:
         for k in range(K):
             ply(graphed, k, acts_g)
     torch.cuda.synchronize()
+    assert slot == 1 and graphed.ply_counter == 0 and graphed.sample_counter == 0  # eager counters untouched
+    base = graphed.graph_counter_base(slot)
     prev = None
-    for _ in range(3):
-        with eager.graph_region():  # outside a capture: enqueues nothing
-            for k in range(K):
-                ply(eager, k, acts_e)
+    for r in range(3):
+        _set_counters(eager, base + r * K)
+        for k in range(K):
+            ply(eager, k, acts_e)
         graph.replay()
         torch.cuda.synchronize()
         assert torch.equal(acts_g, acts_e)
@@ -106,10 +114,97 @@ def test_graph_region_fresh_draws(torch_gpu, n):
         if prev is not None:
             assert not torch.equal(prev, acts_g)  # fresh draws per replay
         prev = acts_g.clone()
-    # the device offsets hold what the replays consumed
-    assert graphed.counter_offsets() == (3 * K, 3 * K)
-    assert eager.counter_offsets() == (0, 0)
+    assert graphed.graph_offsets(slot) == (3 * K, 3 * K)
+    assert graphed.graph_offsets(0) == (0, 0)  # the eager slot never moves
     assert np.array_equal(graphed.counts().cpu().numpy(), eager.counts().cpu().numpy())
+
+
+def test_graph_regions_mixed_with_eager_plies_never_reuse_counters(torch_gpu):
+    """Two graphs of different lengths replayed in alternation with eager plies
+    in between: every launch equals a twin run eagerly at the
+    counters the design assigns (eager: the host counter; graph k: its own
+    range), and the counter intervals used are pairwise disjoint, so no
+    (env id, counter, purpose) Philox key repeats."""
+    torch = torch_gpu
+    from gymothelloenv_amd import VecOthelloEnv
+    E, n, K1, K2 = 1024, 8, 3, 5
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(3)
+    logits = torch.randn(E, n * n, device=dev, generator=g)
+    kw = dict(board_size=n, auto_reset=True, initial_rand_steps=4, seed=2, device=dev)
+    env, twin = VecOthelloEnv(E, **kw), VecOthelloEnv(E, **kw)
+    env.reset()
+    twin.reset()
+    out = torch.empty(max(K1, K2), E, dtype=torch.int32, device=dev)
+    ref = torch.empty_like(out)
+
+    def ply(e, k, o):
+        act, _, _ = e.sample_actions(logits, log_probs=False, entropy=False)
+        e.step(act, observe=False)
+        o[k].copy_(act)
+
+    g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g1), env.graph_region() as s1:
+        for k in range(K1):
+            ply(env, k, out)
+    with torch.cuda.graph(g2), env.graph_region() as s2:
+        for k in range(K2):
+            ply(env, k, out)
+    torch.cuda.synchronize()
+    assert (s1, s2) == (1, 2)
+    used = []  # (start, end) counter intervals
+    replays = {s1: 0, s2: 0}
+    host = 0
+    for step in ["e", "e", s1, "e", s2, s1, s2, "e", s1]:
+        if step == "e":
+            _set_counters(twin, host)
+            ply(env, 0, out)
+            ply(twin, 0, ref)
+            used.append((host, host + 1))
+            host += 1
+            torch.cuda.synchronize()
+            assert torch.equal(out[0], ref[0])
+        else:
+            K = K1 if step == s1 else K2
+            c0 = env.graph_counter_base(step) + replays[step] * K
+            (g1 if step == s1 else g2).replay()
+            _set_counters(twin, c0)
+            for k in range(K):
+                ply(twin, k, ref)
+            used.append((c0, c0 + K))
+            replays[step] += 1
+            torch.cuda.synchronize()
+            assert torch.equal(out[:K], ref[:K])
+        for x, y in zip(env.get_state(), twin.get_state()):
+            assert torch.equal(x, y)
+    used.sort()
+    assert all(a[1] <= b[0] for a, b in zip(used, used[1:]))  # disjoint counter ranges
+    assert env.ply_counter == host and env.sample_counter == host
+    assert env.graph_offsets(s1) == (3 * K1, 3 * K1) and env.graph_offsets(s2) == (2 * K2, 2 * K2)
+    # a state_dict round trip restores the eager counters and leaves the graphs' ranges alone
+    sd = env.state_dict()
+    env.load_state_dict(sd)
+    assert env.ply_counter == host and env.graph_offsets(s1) == (3 * K1, 3 * K1)
+
+
+def test_graph_region_misuse_raises(torch_gpu):
+    """Reversed nesting (region around the capture) and a reset-only region
+    with random openings are refused instead of replaying frozen draws."""
+    torch = torch_gpu
+    from gymothelloenv_amd import VecOthelloEnv
+    env = VecOthelloEnv(256, board_size=6, auto_reset=True, initial_rand_steps=4, device="cuda:0")
+    with pytest.raises(RuntimeError, match="inside torch.cuda.graph"):
+        with env.graph_region():
+            pass
+    g = torch.cuda.CUDAGraph()
+    with pytest.raises(RuntimeError, match="only resets"):
+        with torch.cuda.graph(g), env.graph_region():
+            env.reset()
+    torch.cuda.synchronize()
+    # the handle is usable afterwards: no region left open, eager counters intact
+    assert env.ply_counter == 0
+    env.step_policy("random", n_plies=3)
+    assert env.ply_counter == 3
 
 
 def test_graph_region_step_vs_random_opponent(torch_gpu):
@@ -137,11 +232,13 @@ def test_graph_region_step_vs_random_opponent(torch_gpu):
         out[k, 2].copy_(p)
 
     graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph), graphed.graph_region():
+    with torch.cuda.graph(graph), graphed.graph_region() as slot:
         for k in range(K):
             ply(graphed, k, out_g)
     torch.cuda.synchronize()
-    for _ in range(4):  # 24 calls, about 48 plies: 6x6 games end and auto-reset
+    ended = 0
+    for r in range(4):  # 24 calls, about 48 plies: 6x6 games end and auto-reset
+        _set_counters(eager, graphed.graph_counter_base(slot) + r * K)
         for k in range(K):
             ply(eager, k, out_e)
         graph.replay()
@@ -149,4 +246,5 @@ def test_graph_region_step_vs_random_opponent(torch_gpu):
         assert torch.equal(out_g, out_e)
         for x, y in zip(graphed.get_state(), eager.get_state()):
             assert torch.equal(x, y)
-    assert int(out_e[:, 1].sum()) > 0  # games ended in the last replay (auto-reset with random openings)
+        ended += int(out_e[:, 1].sum())
+    assert ended > 0  # games ended and auto-reset with random openings inside replays

@@ -210,3 +210,57 @@ def test_env_rollout_with_sampled_actions(torch_gpu):
         np.testing.assert_array_equal(b.cpu().numpy().view(np.uint64), s.boards)
         np.testing.assert_array_equal(lg.cpu().numpy().view(np.uint64), s.legal)
     assert (s.meta & 2).all()  # every game finished within 70 plies, none by an illegal move
+
+
+@pytest.mark.parametrize("n_board", [6, 8])
+def test_masked_matches_reference_policy_heads(torch_gpu, golden_dir, n_board):
+    """k_masked against the reference's own policy heads on fixed logits
+    (tests/golden/masked.npz, made by gen_golden.py from model.py / ppo.py):
+    Policy.act's mode and log-probs (model.py:60-99), the log-probs of
+    Policy.act's torch samples, Policy.evaluate_actions' log-probs and
+    unmasked entropy (:156-178), PPO.get_action's renormalised probabilities
+    and its np.random.choice draw for the recorded uniform (ppo.py:228-262).
+    fp32 kernel vs the reference's fp32 torch / float64 numpy: atol 2e-5 +
+    rtol 1e-5; a sampled square may differ only where u lies within 1e-5 of a
+    cumulative-probability boundary (u is rounded to fp32 for the kernel)."""
+    import os
+    torch = torch_gpu
+    from gymothelloenv_amd import masked_log_prob, masked_sample
+    d = np.load(os.path.join(golden_dir, "masked.npz"))
+    k = "N%d_" % n_board
+    logits, nl = d[k + "logits"], d[k + "nlegal"]
+    R, nn = logits.shape
+    dl = torch.from_numpy(logits).cuda()
+    dg = torch.from_numpy(d[k + "legal"].view(np.int64)).cuda()
+    # Policy.act(deterministic=True)
+    a, lp, _ = masked_sample(dl, dg, n_board, mode="mode")
+    np.testing.assert_array_equal(a.cpu().numpy(), d[k + "mode_action"])
+    np.testing.assert_allclose(lp.cpu().numpy(), d[k + "mode_logp"], atol=ATOL, rtol=RTOL)
+    # Policy.act(deterministic=False): log-prob of the reference's own samples
+    lp, _ = masked_log_prob(dl, dg, torch.from_numpy(d[k + "sample_action"]).cuda(), n_board, entropy=False)
+    np.testing.assert_allclose(lp.cpu().numpy(), d[k + "sample_logp"], atol=ATOL, rtol=RTOL)
+    # Policy.evaluate_actions: log-probs (0 off the choices) and dist.entropy() of the unmasked head
+    lp, ent = masked_log_prob(dl, dg, torch.from_numpy(d[k + "eval_action"]).cuda(), n_board, full_entropy=True)
+    np.testing.assert_allclose(lp.cpu().numpy(), d[k + "eval_logp"], atol=ATOL, rtol=RTOL)
+    np.testing.assert_allclose(ent.cpu().numpy(), d[k + "full_entropy"], atol=ATOL, rtol=RTOL)
+    # PPO.get_action: probabilities renormalised over possible_moves
+    words = d[k + "legal"]
+    probs = np.zeros((R, nn))
+    for sq in range(nn):
+        lp_sq, _ = masked_log_prob(dl, dg, torch.full((R,), sq, dtype=torch.int32, device="cuda"), n_board,
+                                   entropy=False)
+        is_legal = ((words[:, sq // 64] >> np.uint64(sq % 64)) & np.uint64(1)).astype(bool)
+        probs[:, sq] = np.where(is_legal, np.exp(lp_sq.cpu().numpy().astype(np.float64)), 0.0)
+    live = nl > 0
+    np.testing.assert_allclose(probs[live], d[k + "ppo_probs"][live], atol=ATOL, rtol=RTOL)
+    # ... and np.random.choice's draw for the recorded uniform
+    u = d[k + "ppo_u"]
+    a, _, _ = masked_sample(dl, dg, n_board, uniforms=torch.from_numpy(u.astype(np.float32)).cuda(),
+                            log_probs=False, entropy=False)
+    a = a.cpu().numpy()
+    ref = d[k + "ppo_action"]
+    bad = np.flatnonzero(live & (a != ref))
+    assert len(bad) <= R // 100, len(bad)
+    for i in bad:
+        cdf = np.cumsum(d[k + "ppo_probs"][i])
+        assert np.min(np.abs(cdf - u[i])) < CDF_TOL, (i, a[i], ref[i])

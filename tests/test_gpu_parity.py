@@ -199,6 +199,34 @@ def test_greedy_rollout_replays_on_oracle(torch_cuda, n, init_rand):
     np.testing.assert_array_equal(env.counts().cpu().numpy(), owdl)
 
 
+@pytest.mark.parametrize("n,policy,init_rand,plies", [(8, "greedy", 10, 140), (6, "random", 0, 80),
+                                                      (10, "random", 0, 200)])
+def test_configs_at_stated_size_replay_on_oracle(torch_cuda, n, policy, init_rand, plies):
+    """Configs 3 and 5 at their stated 65,536 boards (BASELINE.json configs[2],
+    configs[4]): greedy vs greedy after 0..10-ply random openings at 8x8, random
+    play at 6x6 and 10x10; every action, reward, done, the final state and the
+    W/D/L tally equal the oracle's replay (run on host threads)."""
+    torch = torch_cuda
+    E = 65536
+    env = make_env(torch, E, n, auto=True, seed=21, init_rand=init_rand)
+    env.reset()
+    acts, rews, dones = env.step_policy(policy, n_plies=plies)
+    b, m, lg = get_state_np(env)
+    wdl = env.counts().cpu().numpy()
+    s = oracle.reset_openings(n, E, 21, 0, 0, init_rand) if init_rand else oracle.reset(n, E)
+    pid = 0 if policy == "random" else 1
+    oa, orw, od, owdl = oracle.rollout_parallel(s, flags_of(True, False, True), pid, plies, seed=21,
+                                                initial_rand_steps=init_rand)
+    np.testing.assert_array_equal(acts.cpu().numpy(), oa)
+    np.testing.assert_array_equal(rews.cpu().numpy(), orw)
+    np.testing.assert_array_equal(dones.cpu().numpy(), od)
+    np.testing.assert_array_equal(b, s.boards)
+    np.testing.assert_array_equal(m, s.meta)
+    np.testing.assert_array_equal(lg, s.legal)
+    np.testing.assert_array_equal(wdl, owdl)
+    assert owdl.sum() >= E
+
+
 @pytest.mark.parametrize("n", SIZES)
 def test_greedy_actions_match_reference(torch_cuda, golden_dir, n):
     torch = torch_cuda
