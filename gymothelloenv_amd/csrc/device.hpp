@@ -991,6 +991,167 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
     tally(wdl, cb, cd, cw);
 }
 
+#ifndef OTH_FAST_RANDOM
+#define OTH_FAST_RANDOM 1  // k_play_rand: the headline random play (N <= 8, auto-reset, all outputs stored)
+#endif
+
+// k_play_rand: oth_step_policy(RANDOM) on one-word boards with auto-reset and
+// every per-ply output stored -- the benchmark configuration -- with the
+// same results as k_play<N, RANDOM, Fills<N>, true>, restructured for one
+// wave per SIMD, where every VALU instruction of every path a lane of the
+// wave takes is paid by the whole wave:
+//   * the board is held as (mover, opponent) plus the side-to-move bit, so a
+//     ply swaps two words once instead of selecting mover / opponent from
+//     (black, white) and writing them back (othello.py:412-462 flips the
+//     `player_turn`, not the board);
+//   * with auto-reset no board is terminated at a ply's start, so there is no
+//     per-ply "terminated?" branch and no branch-join copies of the carried
+//     fills (a wave holding a board loaded terminated runs k_play's body);
+//   * the opponent's legal scan runs unconditionally (on a full board it
+//     finds nothing: no empty square); only a pass re-scans, in place.
+// The random pick is always legal, so sudden death never triggers here.
+template <int N>
+__device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_t& L, uint32_t& meta,
+                                               const Fills<N>& eng, uint32_t u, uint32_t flags, const Rng& rng,
+                                               uint32_t id, uint64_t g, int& a, int& r, int& d, uint32_t& cb,
+                                               uint32_t& cd, uint32_t& cw) {
+    constexpr uint64_t BD = Geo<N>::BOARD.w[0];
+    constexpr int NN = N * N;
+    a = select64(L, scale_index(u, popc64(L)));  // RandomPolicy (simple_policies.py:37-41); L != 0
+    meta -= (meta & 0xff00u) ? (1u << M_RAND_SHIFT) : 0u;  // a random-opening ply used up
+    const uint64_t m = 1ull << a;
+    BB<1> dummy;
+    dummy.w[0] = 0;
+    const uint64_t f = eng.flip(dummy, dummy, a).w[0];  // update_board (othello.py:391-410)
+    const uint64_t Mn = M | f | m, On = O & ~f;
+    const bool full = (Mn | On) == BD;  // :425-426
+    BB<1> pb, ob;
+    pb.w[0] = On;
+    ob.w[0] = Mn;
+    uint64_t Ln = eng.legal(pb, ob).w[0];  // the opponent's possible_moves (:436), fills kept in eng.t
+    const bool pass = Ln == 0 && !full;
+    if (pass) {  // :437-440: the mover moves again (fills recomputed for the mover)
+        pb.w[0] = Mn;
+        ob.w[0] = On;
+        Ln = eng.legal(pb, ob).w[0];
+    }
+    const bool term = full || Ln == 0;  // full board or nobody can move (:441-442)
+    const bool swap = !pass && !full;
+    M = swap ? On : Mn;
+    O = swap ? Mn : On;
+    L = Ln;
+    meta ^= swap ? M_TURN_WHITE : 0u;
+    r = 0;
+    d = term ? 1 : 0;
+    if (term) {
+        const bool tw = (meta & M_TURN_WHITE) != 0;  // the side that just moved (the turn is not passed on)
+        const int pc = popc64(Mn), oc = popc64(On);
+        if (flags & OTH_DISK_REWARD) r = oc == 0 ? NN : pc - oc;  // :446-459
+        else r = pc > oc ? 1 : (pc < oc ? -1 : 0);                  // winner * player_turn
+        const bool mover_wins = pc > oc, opp_wins = pc < oc;
+        cb += tw ? opp_wins : mover_wins;
+        cd += !mover_wins && !opp_wins;
+        cw += tw ? mover_wins : opp_wins;
+        // auto-reset (othello.py:256-271): black to move from the start position
+        M = Start<N>::BLACK.w[0];
+        O = Start<N>::WHITE.w[0];
+        BB<1> sb, sw;
+        sb.w[0] = M;
+        sw.w[0] = O;
+        L = eng.legal(sb, sw).w[0];  // constant: folds to the start position's moves and fills
+        uint32_t rl = 0;
+        if (rng.init_rand > 0)
+            rl = (uint32_t)scale_index(philox_x(rng.seed, id, g, RNG_OPENING_AUTO), rng.init_rand / 2 + 1) * 2u;
+        meta = (rl & 0xffu) << M_RAND_SHIFT;
+    }
+}
+
+template <int N>
+__global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
+                                                     uint64_t* __restrict__ legal, int E, uint32_t flags, int plies,
+                                                     int32_t* __restrict__ actions, int32_t* __restrict__ rewards,
+                                                     uint8_t* __restrict__ dones,
+                                                     unsigned long long* __restrict__ wdl, Rng rng, uint64_t ply0) {
+    static_assert(Geo<N>::W == 1, "one-word boards");
+    ply0 += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
+    __shared__ __attribute__((aligned(16))) uint64_t lds_rays[Fills<N>::RAY_WORDS];
+    fill_rays<N>(lds_rays);
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    uint32_t cb = 0, cd = 0, cw = 0;
+    if (e < E) {
+        const uint32_t id = rng.id_base + (uint32_t)e;
+        const Fills<N> eng(0, lds_rays);
+        Lane<N> s;
+        load_lane<N>(s, boards, meta, legal, e);
+        const bool tw0 = (s.meta & M_TURN_WHITE) != 0;
+        uint64_t M = tw0 ? s.white.w[0] : s.black.w[0];
+        uint64_t O = tw0 ? s.black.w[0] : s.white.w[0];
+        uint64_t L = s.legal.w[0];
+        uint32_t mt = s.meta & (0xff00u | M_TURN_WHITE);
+        eng.prime(s);
+        // a board loaded terminated stays so (k_play's semantics); such a wave
+        // is rare (set_state) and takes the generic loop below
+        const bool slow = __any((s.meta & M_TERMINATED) != 0);
+        int32_t* act_p = actions + e;
+        int32_t* rew_p = rewards + e;
+        uint8_t* done_p = dones + e;
+        auto ply = [&](int p, uint32_t u) __attribute__((always_inline)) {
+            int a, r, d;
+            play_rand_fast<N>(M, O, L, mt, eng, u, flags, rng, id, ply0 + (uint64_t)p, a, r, d, cb, cd, cw);
+            *act_p = a;
+            *rew_p = r;
+            *done_p = (uint8_t)d;
+            act_p += E;
+            rew_p += E;
+            done_p += E;
+        };
+        if (!slow) {
+            int p = 0;
+            while (p < plies) {  // Philox block g/4 serves plies 4k..4k+3 (g uniform: scalar branches)
+                const uint64_t g = ply0 + (uint64_t)p;
+                const U4 d4 = philox4(rng.seed, id, g >> 2, RNG_ACTION);
+                if ((g & 3) == 0 && p + 4 <= plies) {
+                    ply(p, d4.x);
+                    ply(p + 1, d4.y);
+                    ply(p + 2, d4.z);
+                    ply(p + 3, d4.w);
+                    p += 4;
+                } else {
+                    ply(p, pick4(d4, (uint32_t)(g & 3)));
+                    ++p;
+                }
+            }
+            const bool tw = (mt & M_TURN_WHITE) != 0;
+            s.white.w[0] = tw ? M : O;
+            s.black.w[0] = tw ? O : M;
+            s.legal.w[0] = L;
+            s.meta = mt;
+        } else {
+            for (int p = 0; p < plies; ++p) {
+                const uint64_t g = ply0 + (uint64_t)p;
+                int a = -1, r = 0, d = 1, win = NO_DISK;
+                if (!(s.meta & M_TERMINATED)) {
+                    a = random_action<N>(s, action_draw(rng.seed, id, g));
+                    if ((s.meta >> M_RAND_SHIFT) > 0) s.meta -= 1u << M_RAND_SHIFT;
+                    step_lane<N, Fills<N>, true>(s, a, flags, r, d, win, eng);
+                    if (d) {
+                        cb += win == BLACK_DISK;
+                        cd += win == NO_DISK;
+                        cw += win == WHITE_DISK;
+                        reset_lane<N>(s, rng.seed, id, g, RNG_OPENING_AUTO, rng.init_rand);
+                        eng.prime(s);
+                    }
+                }
+                act_p[(size_t)p * E] = a;
+                rew_p[(size_t)p * E] = r;
+                done_p[(size_t)p * E] = (uint8_t)d;
+            }
+        }
+        store_lane<N>(s, boards, meta, legal, e);
+    }
+    tally(wdl, cb, cd, cw);
+}
+
 
 // ---------------------------------------------------------------------------
 // OthelloEnv semantics on the device (othello.py:151-200): the protagonist

@@ -56,6 +56,13 @@ template <int N, int POL, typename Eng>
 void launch_k_play(int lanes_per_board, oth_env* env, int n_plies, int32_t* actions, int32_t* rewards,
                    uint8_t* dones, uint64_t ply0, hipStream_t st) {
     const dim3 grid(grid_for((long long)lanes_per_board * env->E)), block(BLOCK);
+    if constexpr (OTH_FAST_RANDOM && POL == OTH_POLICY_RANDOM && std::is_same<Eng, Fills<N>>::value) {
+        if (actions && rewards && dones && (env->flags & OTH_AUTO_RESET)) {
+            hipLaunchKernelGGL((k_play_rand<N>), grid, block, 0, st, env->boards, env->meta, env->legal, env->E,
+                               env->flags, n_plies, actions, rewards, dones, env->wdl, rng_of(env), ply0);
+            return;
+        }
+    }
     if constexpr (OTH_REC_TEMPLATE && (POL == OTH_POLICY_RANDOM || POL == OTH_POLICY_GREEDY)) {
         if (actions && rewards && dones) {
             hipLaunchKernelGGL((k_play<N, POL, Eng, true>), grid, block, 0, st, env->boards, env->meta, env->legal,

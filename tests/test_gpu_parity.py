@@ -167,6 +167,36 @@ def test_fills_engine_flag_combinations(torch_cuda, n, policy, sd, dr, auto, ini
     np.testing.assert_array_equal(env.counts().cpu().numpy(), owdl)
 
 
+@pytest.mark.parametrize("n", [6, 8])
+def test_random_rollout_with_boards_loaded_terminated(torch_cuda, n):
+    """k_play_rand's fallback: waves holding a board that was loaded
+    terminated (set_state) run the generic ply loop; that board reports
+    action -1 / done 1 every ply and is never reset (oth_step_policy's
+    semantics), every other board of the wave plays on.  Equal to the oracle."""
+    torch = torch_cuda
+    E, plies = 4096, 70
+    env = make_env(torch, E, n, auto=True, seed=13)
+    env.step_policy("random", n_plies=9)
+    b, m, lg = get_state_np(env)
+    m = m.copy()
+    m[::300] |= 2  # terminated (winner bits 0: a draw) in a few waves
+    env.set_state(t64(torch, b), torch.from_numpy(m.view(np.int16)).cuda(), t64(torch, lg))
+    env.counts(reset=True)
+    acts, rews, dones = env.step_policy("random", n_plies=plies)
+    s = oracle.State(n, E)
+    s.boards[:], s.meta[:], s.legal[:] = b, m, lg
+    oa, orw, od, owdl = oracle.rollout(s, flags_of(True, False, True), 0, plies, seed=13, ply0=9)
+    np.testing.assert_array_equal(acts.cpu().numpy(), oa)
+    np.testing.assert_array_equal(rews.cpu().numpy(), orw)
+    np.testing.assert_array_equal(dones.cpu().numpy(), od)
+    b2, m2, lg2 = get_state_np(env)
+    np.testing.assert_array_equal(b2, s.boards)
+    np.testing.assert_array_equal(m2, s.meta)
+    np.testing.assert_array_equal(lg2, s.legal)
+    np.testing.assert_array_equal(env.counts().cpu().numpy(), owdl)
+    assert (oa[:, ::300] == -1).all()
+
+
 def test_rollout_split_over_launches_is_identical(torch_cuda):
     """K plies in one launch == K single-ply launches (state round-trips HBM)."""
     torch = torch_cuda
