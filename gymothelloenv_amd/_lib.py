@@ -53,8 +53,10 @@ SIGNATURES = {
     "oth_set_player_turn": (_I32, [_P, _I32, _P, _P]),
     "oth_count_disks": (_I32, [_P, _P, _P]),
     "oth_counts": (_I32, [_P, _P, _I32, _P]),
+    "oth_counts_vs": (_I32, [_P, _P, _I32, _P]),
     "oth_masked_sample": (_I32, [_I32, _I32, _P, _I64, _P, _P, _U64, _U32, _U64, _I32, _P, _P, _P, _P]),
     "oth_sample_actions": (_I32, [_P, _P, _I64, _P, _U64, _I32, _P, _P, _P, _P]),
+    "oth_sample_step": (_I32, [_P, _P, _I64, _P, _U64, _I32, _P, _P, _P, _P, _P, _P]),
     "oth_ply_counter": (_U64, [_P]),
     "oth_set_ply_counter": (_I32, [_P, _U64]),
     "oth_graph_begin": (_I32, [_P, _P]),
@@ -107,9 +109,10 @@ def load_path(path):
     import torch  # noqa: F401
     lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
-        fn.restype = res
-        fn.argtypes = args
+        fn = getattr(lib, name, None)  # an older variant may lack newer entry points
+        if fn is not None:
+            fn.restype = res
+            fn.argtypes = args
     return lib
 
 

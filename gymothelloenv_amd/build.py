@@ -23,7 +23,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 SIZES = list(range(4, 17))
-SOURCES = ("capi.hip", "kernels_n.hip", "masked.hip", "device.hpp", "launch.hpp", "bitboard.hpp")
+SOURCES = ("capi.hip", "kernels_n.hip", "masked.hip", "device.hpp", "launch.hpp", "bitboard.hpp", "masked.hpp")
 DEPS = [os.path.join(CSRC, f) for f in SOURCES] + [os.path.join(ROOT, "include", "othello_mi355x.h")]
 OUT = os.path.join(HERE, "liboth_mi355x.so")
 OBJDIR = os.path.join(HERE, "_objs")

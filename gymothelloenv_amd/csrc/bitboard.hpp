@@ -130,6 +130,17 @@ OTH_HD int clz64(uint64_t x) {  // x != 0
     return __builtin_clzll(x);
 #endif
 }
+// Bit reversal of a 64-bit word (bit a -> bit 63 - a): two v_bfrev_b32 on the device.
+OTH_HD uint64_t rev64(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__clang__)
+    return __builtin_bitreverse64(x);
+#else
+    x = __builtin_bswap64(x);
+    x = ((x >> 4) & 0x0F0F0F0F0F0F0F0Full) | ((x & 0x0F0F0F0F0F0F0F0Full) << 4);
+    x = ((x >> 2) & 0x3333333333333333ull) | ((x & 0x3333333333333333ull) << 2);
+    return ((x >> 1) & 0x5555555555555555ull) | ((x & 0x5555555555555555ull) << 1);
+#endif
+}
 template <int W>
 OTH_HD int popcount(const BB<W>& a) {
     int c = 0;
@@ -734,6 +745,10 @@ OTH_HD BB<Geo<N>::W> flips(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O, const
 // t[d] = the fill of ray direction d: opponent discs from which an own disc is
 // reached going along d through opponent discs only.  The run a move on square
 // a flips along d is the contiguous part of ray d from a inside t[d].
+#ifndef OTH_CARRY_H
+#define OTH_CARRY_H 1  // OneWord: the horizontal axis of the legal scan by carry chains (axis_h)
+#endif
+
 template <int N>
 struct OneWord {
     static_assert(Geo<N>::W == 1, "one-word boards (N <= 8)");
@@ -764,12 +779,36 @@ struct OneWord {
         tminus = x;
         L = L | sh<-S>(x);
     }
+    // Square a -> square NN-1-a: the board turned by 180 degrees (a row stays
+    // a row, reversed), an involution on the board's NN bits.
+    static OTH_HD uint64_t turn180(uint64_t x) { return rev64(x) >> (64 - N * N); }
+
+    // The horizontal axis by carries (OTH_CARRY_H): stepping +1 from an own
+    // disc through a run of opponent discs of the inner columns is a carry
+    // chain of (P << 1) + pin, which clears the run and sets the square past
+    // it, so the fill is pin & ~((P << 1) + pin) -- one v_lshl_add_u64 and an
+    // and-not instead of the doubling steps (no carry crosses a row: pin has
+    // no edge-column square).  Stepping -1 is the same on the board turned by
+    // 180 degrees.  tplus / tminus as in axis<1>.
+    static OTH_HD void axis_h(uint64_t P, uint64_t pin, U2& L, U2& tplus, U2& tminus) {
+        const uint64_t fe = pin & ~((P << 1) + pin);
+        const uint64_t rpin = turn180(pin);
+        const uint64_t fw = turn180(rpin & ~((turn180(P) << 1) + rpin));
+        tplus = u2(fe);
+        tminus = u2(fw);
+        L = L | u2((fe << 1) | (fw >> 1));
+    }
+
     // get_possible_actions (othello.py:313-343) for the mover P against O,
     // with the eight fills stored in t.
     static OTH_HD uint64_t legal(uint64_t Pw, uint64_t Ow, uint64_t t[8]) {
         const U2 P = u2(Pw), O = u2(Ow), pin = O & u2(IN);
         U2 L{0u, 0u}, f[8];
+#if OTH_CARRY_H
+        axis_h(Pw, Ow & IN, L, f[4], f[0]);
+#else
         axis<1>(P, pin, L, f[4], f[0]);
+#endif
         axis<N>(P, O, L, f[5], f[1]);
         axis<N + 1>(P, pin, L, f[6], f[2]);
         axis<N - 1>(P, pin, L, f[7], f[3]);

@@ -156,6 +156,8 @@ int oth_create(int32_t n_envs, int32_t board_size, uint32_t flags, uint64_t seed
     const size_t slot_bytes = (size_t)env->nslots * 4 * sizeof(unsigned long long);
     if (err == hipSuccess) err = hipMalloc((void**)&env->wdl, slot_bytes);
     if (err == hipSuccess) err = hipMemset(env->wdl, 0, slot_bytes);
+    if (err == hipSuccess) err = hipMalloc((void**)&env->wdl_vs, slot_bytes);
+    if (err == hipSuccess) err = hipMemset(env->wdl_vs, 0, slot_bytes);
     const size_t ctr_bytes = (size_t)OTH_GRAPH_SLOTS * 2 * sizeof(uint64_t);
     if (err == hipSuccess) err = hipMalloc((void**)&env->ctr_slots, ctr_bytes);
     if (err == hipSuccess) err = hipMemset(env->ctr_slots, 0, ctr_bytes);
@@ -186,6 +188,7 @@ int oth_destroy(oth_env* env) {
     if (env->meta) (void)hipFree(env->meta);
     if (env->legal) (void)hipFree(env->legal);
     if (env->wdl) (void)hipFree(env->wdl);
+    if (env->wdl_vs) (void)hipFree(env->wdl_vs);
     if (env->ctr_slots) (void)hipFree(env->ctr_slots);
     delete env;
     return OTH_OK;
@@ -302,6 +305,21 @@ int oth_sample_actions(oth_env* env, const float* logits, int64_t ld, const floa
                          env->cur_off + 1, mode, actions, log_probs, entropy, (hipStream_t)stream);
 }
 
+int oth_sample_step(oth_env* env, const float* logits, int64_t ld, const float* uniforms, uint64_t counter,
+                    int32_t mode, int32_t* actions, float* log_probs, float* entropy, int32_t* rewards, uint8_t* dones,
+                    oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    if (!logits || !actions) return fail(OTH_EINVAL, "logits / actions is NULL");
+    const int base = mode & ~OTH_MASKED_FULL_ENTROPY;
+    if (base != OTH_MASKED_SAMPLE && base != OTH_MASKED_MODE) return fail(OTH_EINVAL, "mode must be SAMPLE or MODE");
+    if (ld < (int64_t)env->n * env->n) return fail(OTH_EINVAL, "ld < N*N");
+    const uint64_t ply = env->ply++;
+    return with_n(env->n, [&](auto NC) {
+        return launch_sample_step<decltype(NC)::value>(env, logits, (long long)ld, uniforms, counter, mode, actions,
+                                                       log_probs, entropy, rewards, dones, ply, (hipStream_t)stream);
+    });
+}
+
 // A graph region's offsets move on by what one replay consumed (enqueued as
 // the region's last node, so every replay advances them).
 __global__ void k_graph_advance(uint64_t* __restrict__ off, uint64_t d_ply, uint64_t d_sample) {
@@ -406,6 +424,14 @@ int oth_counts(oth_env* env, int64_t* out, int32_t reset, oth_stream_t stream) {
     if (reset) OTH_HIP(hipMemsetAsync(env->wdl, 0, 4 * sizeof(unsigned long long), s));
     return OTH_OK;
 #endif
+}
+
+int oth_counts_vs(oth_env* env, int64_t* out, int32_t reset, oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    if (!out) return fail(OTH_EINVAL, "out is NULL");
+    hipLaunchKernelGGL(k_reduce_wdl, dim3(1), dim3(256), 0, (hipStream_t)stream, env->wdl_vs, env->nslots, out,
+                       reset ? 1 : 0);
+    return after_launch("oth_counts_vs");
 }
 
 uint64_t oth_ply_counter(const oth_env* env) { return env ? env->ply : 0; }

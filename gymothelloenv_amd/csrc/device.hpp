@@ -25,6 +25,7 @@
 #include <type_traits>
 
 #include "bitboard.hpp"
+#include "masked.hpp"
 #include "othello_mi355x.h"
 
 using namespace oth;
@@ -76,6 +77,12 @@ using namespace oth;
 #endif
 #ifndef OTH_FLIP_AND3
 #define OTH_FLIP_AND3 1  // Fills::flip toward higher squares as one 3-input AND (v_bitop3_b32) per dword
+#endif
+#ifndef OTH_SS_STAGE
+#define OTH_SS_STAGE 0  // 1: k_sample_step stages the wave's logits rows through LDS (coalesced loads; measured slower: 8.6 -> 11.1 us per ply at 8x8)
+#endif
+#ifndef OTH_FLIP_TURN
+#define OTH_FLIP_TURN 0  // 1: Fills::flip toward lower squares on the board turned by 180 degrees (no 64-bit clz; measured -1.5 % at 8x8, -3 % at 6x6)
 #endif
 #ifndef OTH_DRAW_UNROLL
 #define OTH_DRAW_UNROLL 1  // k_play random: four plies unrolled per Philox block (no per-ply word rotation)
@@ -346,6 +353,22 @@ struct Fills {
             f |= ray & ((y & (0ull - y)) - 1ull);
 #endif
         }
+#if OTH_FLIP_TURN
+        // toward lower squares on the board turned by 180 degrees (square s ->
+        // NN-1-s, OneWord::turn180): ray d from a becomes ray d-4 from NN-1-a,
+        // toward higher squares, so the same lowest-bit form applies to the
+        // turned fill; one turn of the or-ed runs at the end
+        const uint64_t* rt = rays + (N * N - 1 - a);
+        uint64_t g = 0;
+#pragma unroll
+        for (int d = 4; d < 8; ++d) {
+            const uint64_t ray = rt[64 * (d - 4)];
+            const uint64_t tt = OneWord<N>::turn180(t[d]);
+            const uint64_t y = ray & ~tt;
+            g |= and3_64(ray, tt, y - 1ull);
+        }
+        f |= OneWord<N>::turn180(g);
+#else
 #pragma unroll
         for (int d = 4; d < 8; ++d) {  // toward lower squares: cap = highest ray square outside the fill
             // y == 0 only when the ray is empty (the edge square of a ray is never in a fill)
@@ -354,6 +377,7 @@ struct Fills {
             const uint64_t hb = 0x8000000000000000ull >> __clzll(y);
             f |= ray & (0ull - (hb << 1));
         }
+#endif
         BB<1> out;
         out.w[0] = f;
         return out;
@@ -1153,6 +1177,98 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
 }
 
 
+// oth_sample_step: the learners' per-ply loop in one launch -- the masked
+// categorical over each board's possible_moves (Policy.act, model.py:60-99;
+// PPO.get_action, ppo.py:228-262) immediately followed by OthelloBaseEnv.step
+// (othello.py:412-462) with the sampled action.  The sampling runs the very
+// code of k_masked (masked.hpp) with its G lanes per board: lane group g
+// samples its G boards g*G .. g*G+G-1 one after the other and lane l keeps
+// board g*G+l's pick, which is the board it then steps (one lane per board,
+// as k_step).  So the results are bit-identical to oth_sample_actions +
+// oth_step, with one launch and no actions round trip through memory.
+// ONE (boards of up to two words): each lane samples its own board with
+// oth_ms::sample_lane, the group's arithmetic restated for one lane.
+template <int N, int G, bool VEC, bool FULL, bool ONE>
+__global__ __launch_bounds__(BLOCK) void k_sample_step(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
+                                                       uint64_t* __restrict__ legal, int E, uint32_t flags,
+                                                       const float* __restrict__ logits, long long ld,
+                                                       const float* __restrict__ uniforms, uint64_t counter, int mode,
+                                                       int32_t* __restrict__ actions, float* __restrict__ log_probs,
+                                                       float* __restrict__ entropy, int32_t* __restrict__ rewards,
+                                                       uint8_t* __restrict__ dones,
+                                                       unsigned long long* __restrict__ wdl, Rng rng, uint64_t ply) {
+    constexpr int NN = N * N;
+    constexpr int CH = Geo<N>::W;
+    ply += rng.ply_off[0];      // graph-region offsets (oth_graph_end); 0 eagerly
+    counter += rng.ply_off[1];  // the sample counter's, as k_masked
+    const long long t = (long long)blockIdx.x * BLOCK + threadIdx.x;
+    const int l = (int)(t % G);
+    const long long g0 = (t / G) * G;
+    const bool mine_live = t < E;
+    // the board this lane steps: its loads are issued before the sampling, so
+    // they are in flight while the group samples
+    Lane<N> s;
+    if (mine_live) load_lane<N>(s, boards, meta, legal, (int)t);
+    oth_ms::Pick mine{0, 0.f, 0.f};
+    if constexpr (ONE) {  // one lane per board: the group's arithmetic restated per lane (oth_ms::sample_lane)
+        const oth_ms::f32x4* row = nullptr;
+        if constexpr (VEC && OTH_SS_STAGE) {  // the wave's 64 rows through LDS: coalesced loads
+            constexpr int QN = NN / 4;
+            __shared__ oth_ms::f32x4 stage[(BLOCK / 64) * 64 * (QN + 1)];
+            const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+            oth_ms::f32x4* ws = stage + wv * 64 * (QN + 1);
+            oth_ms::stage_rows<QN>(ws, t - lane, E, logits, ld, lane);
+            __syncthreads();
+            row = ws + lane * (QN + 1);
+        }
+        if (mine_live)
+            mine = oth_ms::sample_lane<CH, G, VEC, FULL>((int)t, NN, logits, ld, legal, uniforms, rng.seed,
+                                                         rng.id_base, counter, mode, 0, log_probs != nullptr,
+                                                         entropy != nullptr, row);
+    } else {
+    constexpr int BATCH = G < 4 ? G : 4;  // boards whose logits loads are issued together
+#pragma unroll 1
+    for (int k0 = 0; k0 < G; k0 += BATCH) {
+        oth_ms::Slot<CH, G> b[BATCH];
+#pragma unroll
+        for (int k = 0; k < BATCH; ++k) {
+            const long long eb = g0 + k0 + k;
+            b[k].live = eb < E;
+            b[k].e = b[k].live ? (int)eb : E - 1;  // dead boards still take part in the group's DPP steps
+            oth_ms::load_slot<CH, G, VEC>(b[k], l, NN, logits, ld, legal);
+        }
+#pragma unroll
+        for (int k = 0; k < BATCH; ++k) {
+            const oth_ms::Pick pk = oth_ms::finish_slot<CH, G, FULL>(b[k], l, NN, logits, ld, uniforms, rng.seed,
+                                                                     rng.id_base, counter, mode, 0,
+                                                                     log_probs != nullptr, entropy != nullptr);
+            if (k0 + k == l) mine = pk;
+        }
+    }
+    }
+    uint32_t cb = 0, cd = 0, cw = 0;
+    if (mine_live) {
+        const int e = (int)t;
+        actions[e] = mine.a;
+        if (log_probs) log_probs[e] = mine.lp;
+        if (entropy) entropy[e] = mine.ent;
+        const bool was_term = (s.meta & M_TERMINATED) != 0;
+        int r, d, win;
+        step_lane<N>(s, mine.a, flags, r, d, win, Solo<N>(0, nullptr));
+        if (d && !was_term) {
+            cb = win == BLACK_DISK;
+            cd = win == NO_DISK;
+            cw = win == WHITE_DISK;
+            if (flags & OTH_AUTO_RESET)
+                reset_lane<N>(s, rng.seed, rng.id_base + (uint32_t)e, ply, RNG_OPENING_AUTO, rng.init_rand);
+        }
+        store_lane<N>(s, boards, meta, legal, e);
+        if (rewards) rewards[e] = r;
+        if (dones) dones[e] = (uint8_t)d;
+    }
+    tally(wdl, cb, cd, cw);
+}
+
 // ---------------------------------------------------------------------------
 // OthelloEnv semantics on the device (othello.py:151-200): the protagonist
 // steps with the caller's action, then the embedded opponent (random or greedy,
@@ -1214,10 +1330,11 @@ __global__ __launch_bounds__(BLOCK) void k_step_vs(uint64_t* __restrict__ boards
                                                    const int32_t* __restrict__ actions, const int8_t* __restrict__ prot,
                                                    int32_t* __restrict__ rewards, uint8_t* __restrict__ dones,
                                                    int32_t* __restrict__ plies_out,
-                                                   unsigned long long* __restrict__ wdl, Rng rng, uint64_t call) {
+                                                   unsigned long long* __restrict__ wdl,
+                                                   unsigned long long* __restrict__ wdl_vs, Rng rng, uint64_t call) {
     call += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
     const int e = blockIdx.x * BLOCK + threadIdx.x;
-    uint32_t cb = 0, cd = 0, cw = 0;
+    uint32_t cb = 0, cd = 0, cw = 0, pw_n = 0, pd_n = 0, pl_n = 0;
     if (e < E) {
         const uint32_t id = rng.id_base + (uint32_t)e;
         const bool pw = prot ? prot[e] == WHITE_DISK : true;
@@ -1253,6 +1370,12 @@ __global__ __launch_bounds__(BLOCK) void k_step_vs(uint64_t* __restrict__ boards
                 cb = win == BLACK_DISK;
                 cd = win == NO_DISK;
                 cw = win == WHITE_DISK;
+                // the harnesses' count from the protagonist's final reward (run.py:100-130:
+                // its sign is the protagonist's result in both reward modes)
+                const int pcol = pw ? WHITE_DISK : BLACK_DISK;
+                pw_n = win == pcol;
+                pd_n = win == NO_DISK;
+                pl_n = win == -pcol;
                 if (flags & OTH_AUTO_RESET) reset_vs_lane<N, POLICY>(s, pw, flags, rng, id, call, RNG_OPENING_AUTO, j);
             }
         }
@@ -1262,6 +1385,7 @@ __global__ __launch_bounds__(BLOCK) void k_step_vs(uint64_t* __restrict__ boards
         if (plies_out) plies_out[e] = plies;
     }
     tally(wdl, cb, cd, cw);
+    tally(wdl_vs, pw_n, pd_n, pl_n);
 }
 
 template <int N>

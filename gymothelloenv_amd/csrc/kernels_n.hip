@@ -99,6 +99,45 @@ int launch_play(oth_env* env, int policy, int n_plies, int32_t* actions, int32_t
     });
 }
 
+#ifndef OTH_SS_ONE
+#define OTH_SS_ONE 1  // oth_sample_step: one lane samples one board (oth_ms::sample_lane) for boards of <= 2 words
+#endif
+
+template <int N, int G, bool VEC, bool FULL>
+void launch_ss(oth_env* env, const float* logits, long long ld, const float* uniforms, uint64_t counter, int mode,
+               int32_t* actions, float* log_probs, float* entropy, int32_t* rewards, uint8_t* dones, uint64_t ply,
+               hipStream_t st) {
+    constexpr bool ONE = OTH_SS_ONE && Geo<N>::W <= 2;
+    const long long lanes = ONE ? (long long)env->E : ((long long)env->E + G - 1) / G * G;
+    hipLaunchKernelGGL((k_sample_step<N, G, VEC, FULL, ONE>), dim3(grid_for(lanes)), dim3(BLOCK), 0, st, env->boards,
+                       env->meta, env->legal, env->E, env->flags, logits, ld, uniforms, counter, mode, actions,
+                       log_probs, entropy, rewards, dones, env->wdl, rng_of(env), ply);
+}
+
+// the sampler's lanes per board: k_masked's choice for the board's word count
+// (launch_masked), so the arithmetic is the same instruction for instruction
+template <int N>
+int launch_sample_step(oth_env* env, const float* logits, long long ld, const float* uniforms, uint64_t counter,
+                       int mode, int32_t* actions, float* log_probs, float* entropy, int32_t* rewards, uint8_t* dones,
+                       uint64_t ply, hipStream_t st) {
+    constexpr int G = Geo<N>::W <= 2 ? OTH_MS_G : 16;
+    const bool vec = ((N * N) % 4 == 0) && (ld % 4 == 0) && (((uintptr_t)logits & 15u) == 0);
+    const bool full = (mode & OTH_MASKED_FULL_ENTROPY) != 0;
+    const int base = mode & 3;
+    if (vec) {
+        if (full) launch_ss<N, G, true, true>(env, logits, ld, uniforms, counter, base, actions, log_probs, entropy,
+                                              rewards, dones, ply, st);
+        else launch_ss<N, G, true, false>(env, logits, ld, uniforms, counter, base, actions, log_probs, entropy,
+                                          rewards, dones, ply, st);
+    } else {
+        if (full) launch_ss<N, G, false, true>(env, logits, ld, uniforms, counter, base, actions, log_probs,
+                                               entropy, rewards, dones, ply, st);
+        else launch_ss<N, G, false, false>(env, logits, ld, uniforms, counter, base, actions, log_probs, entropy,
+                                           rewards, dones, ply, st);
+    }
+    return after_launch("oth_sample_step");
+}
+
 template <int N>
 int launch_reset_vs(oth_env* env, int policy, const int8_t* prot, const uint8_t* mask, uint64_t call,
                     hipStream_t st) {
@@ -117,7 +156,7 @@ int launch_step_vs(oth_env* env, int policy, const int32_t* actions, const int8_
         constexpr int POL = decltype(PC)::value;
         hipLaunchKernelGGL((k_step_vs<N, POL>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards, env->meta,
                            env->legal, env->E, env->flags, actions, prot, rewards, dones, plies, env->wdl,
-                           rng_of(env), call);
+                           env->wdl_vs, rng_of(env), call);
         return after_launch("oth_step_vs");
     });
 }
@@ -214,6 +253,8 @@ template int launch_play<OTH_N>(oth_env*, int, int, int32_t*, int32_t*, uint8_t*
 template int launch_reset_vs<OTH_N>(oth_env*, int, const int8_t*, const uint8_t*, uint64_t, hipStream_t);
 template int launch_step_vs<OTH_N>(oth_env*, int, const int32_t*, const int8_t*, int32_t*, uint8_t*, int32_t*,
                                    uint64_t, hipStream_t);
+template int launch_sample_step<OTH_N>(oth_env*, const float*, long long, const float*, uint64_t, int, int32_t*,
+                                       float*, float*, int32_t*, uint8_t*, uint64_t, hipStream_t);
 template int launch_policy_actions<OTH_N>(oth_env*, int, int32_t*, hipStream_t);
 template int launch_legal_moves<OTH_N>(int, const uint64_t*, const uint64_t*, uint64_t*, hipStream_t);
 template int launch_observe<OTH_N>(oth_env*, int, int, void*, hipStream_t);

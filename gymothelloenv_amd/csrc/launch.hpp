@@ -20,7 +20,8 @@ struct oth_env {
     uint64_t* boards;
     uint16_t* meta;
     uint64_t* legal;
-    unsigned long long* wdl;  // [nslots][4] per-block W/D/L slots (tally)
+    unsigned long long* wdl;     // [nslots][4] per-block W/D/L slots by colour (tally)
+    unsigned long long* wdl_vs;  // [nslots][4] per-block {protagonist wins, draws, losses} of oth_step_vs
     int32_t nslots;
     // Philox counter offsets (HIP-graph regions, oth_graph_begin/_end):
     // device [OTH_GRAPH_SLOTS][2] = (ply, sample) offsets; slot 0 serves eager
@@ -60,6 +61,10 @@ int launch_reset_vs(oth_env* env, int policy, const int8_t* prot, const uint8_t*
 template <int N>
 int launch_step_vs(oth_env* env, int policy, const int32_t* actions, const int8_t* prot, int32_t* rewards,
                    uint8_t* dones, int32_t* plies, uint64_t call, hipStream_t st);
+template <int N>
+int launch_sample_step(oth_env* env, const float* logits, long long ld, const float* uniforms, uint64_t counter,
+                       int mode, int32_t* actions, float* log_probs, float* entropy, int32_t* rewards, uint8_t* dones,
+                       uint64_t ply, hipStream_t st);
 template <int N> int launch_policy_actions(oth_env* env, int policy, int32_t* out, hipStream_t st);
 template <int N>
 int launch_legal_moves(int n, const uint64_t* mover, const uint64_t* opp, uint64_t* out, hipStream_t st);

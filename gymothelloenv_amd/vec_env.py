@@ -261,6 +261,13 @@ class VecOthelloEnv(object):
         L.check(self._lib.oth_counts(self._h, _ptr(out), int(bool(reset)), self._stream()), "oth_counts")
         return out
 
+    def counts_vs(self, reset=False):
+        """{protagonist wins, draws, protagonist losses} of games finished by
+        step_vs (run.py:100-130's count, the README's table) as int64 (3,)."""
+        out = torch.empty(3, dtype=torch.int64, device=self.device)
+        L.check(self._lib.oth_counts_vs(self._h, _ptr(out), int(bool(reset)), self._stream()), "oth_counts_vs")
+        return out
+
     def sample_actions(self, logits, deterministic=False, uniforms=None, log_probs=True, entropy=True):
         """Policy.act (model.py:60-99) for every board at once: sample (or, when
         deterministic, take the mode of) the softmax of `logits` (E, N*N)
@@ -283,6 +290,31 @@ class VecOthelloEnv(object):
                 "oth_sample_actions")
         self._sample_calls += 1
         return acts, lp, ent
+
+    def sample_step(self, logits, deterministic=False, uniforms=None, log_probs=True, entropy=True,
+                    full_entropy=False, rewards=None, dones=None):
+        """sample_actions(logits) then step(actions) in ONE launch (oth_sample_step):
+        Policy.act (model.py:60-99) over every board's possible_moves followed by
+        OthelloBaseEnv.step (othello.py:412-462), bit-identical to the two calls.
+        Returns (actions int32, log_probs, entropy, rewards int32, dones bool)."""
+        from .masked import _rows
+        x = _rows(logits, self.board_size)
+        if x.shape[0] != self.num_envs:
+            raise ValueError("logits must have one row per board")
+        if uniforms is not None:
+            uniforms = uniforms.to(device=x.device, dtype=torch.float32).contiguous()
+        acts = self._i32(self.num_envs)
+        lp = torch.empty(self.num_envs, dtype=torch.float32, device=self.device) if log_probs else None
+        ent = torch.empty(self.num_envs, dtype=torch.float32, device=self.device) if entropy else None
+        r = rewards if rewards is not None else self._i32(self.num_envs)
+        d = dones if dones is not None else self._u8(self.num_envs)
+        mode = (L.OTH_MASKED_MODE if deterministic else L.OTH_MASKED_SAMPLE) | \
+            (L.OTH_MASKED_FULL_ENTROPY if full_entropy else 0)
+        L.check(self._lib.oth_sample_step(self._h, _ptr(x), x.stride(0), _ptr(uniforms), self._sample_calls, mode,
+                                          _ptr(acts), _ptr(lp), _ptr(ent), _ptr(r), _ptr(d), self._stream()),
+                "oth_sample_step")
+        self._sample_calls += 1
+        return acts, lp, ent, r, d.view(torch.bool)
 
     @property
     def sample_counter(self):

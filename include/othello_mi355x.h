@@ -174,6 +174,12 @@ int oth_count_disks(oth_env *env, int32_t *out, oth_stream_t stream);
  * wins} (device pointer).  reset != 0 zeroes the counters after the copy. */
 int oth_counts(oth_env *env, int64_t *out, int32_t reset, oth_stream_t stream);
 
+/* The harnesses' tally (run.py:100-130, the README's wins / draws / loses) of
+ * games finished by oth_step_vs, from each board's protagonist's side: out
+ * int64[3] = {protagonist wins, draws, protagonist losses} (device pointer);
+ * reset != 0 zeroes the counters after the copy. */
+int oth_counts_vs(oth_env *env, int64_t *out, int32_t reset, oth_stream_t stream);
+
 /* Masked categorical over each board's legal squares (policy head of the
  * learners; replaces the per-sample loops of
  * pytorch_a2c_ppo_acktr_gail/a2c_ppo_acktr/model.py:60-99 Policy.act,
@@ -198,6 +204,18 @@ int oth_masked_sample(int32_t board_size, int32_t n, const float *logits, int64_
  * by the handle's seed and env ids. */
 int oth_sample_actions(oth_env *env, const float *logits, int64_t ld, const float *uniforms, uint64_t counter,
                        int32_t mode, int32_t *actions, float *log_probs, float *entropy, oth_stream_t stream);
+
+/* One ply of the learners' loop in one launch: oth_sample_actions (mode
+ * OTH_MASKED_SAMPLE or OTH_MASKED_MODE, optionally | OTH_MASKED_FULL_ENTROPY)
+ * over the handle's possible_moves, then oth_step with the chosen actions
+ * (Policy.act model.py:60-99 / PPO.get_action ppo.py:228-262, then
+ * OthelloBaseEnv.step othello.py:412-462).  Results are bit-identical to the
+ * two calls.  Out: actions int32[E] (required), log_probs / entropy float[E],
+ * rewards int32[E], dones uint8[E] (each may be NULL).  Advances the ply
+ * counter by one; `counter` is the sample counter as in oth_sample_actions. */
+int oth_sample_step(oth_env *env, const float *logits, int64_t ld, const float *uniforms, uint64_t counter,
+                    int32_t mode, int32_t *actions, float *log_probs, float *entropy, int32_t *rewards,
+                    uint8_t *dones, oth_stream_t stream);
 
 /* Global ply counter of the handle: the Philox counter of the next eager ply
  * (random policy, openings, device opponents).  Host value only; setting it

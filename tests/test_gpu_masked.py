@@ -264,3 +264,69 @@ def test_masked_matches_reference_policy_heads(torch_gpu, golden_dir, n_board):
     for i in bad:
         cdf = np.cumsum(d[k + "ppo_probs"][i])
         assert np.min(np.abs(cdf - u[i])) < CDF_TOL, (i, a[i], ref[i])
+
+
+@pytest.mark.parametrize("n_board,E", [(8, 65536), (6, 3001), (10, 4096), (16, 1000)])
+def test_sample_step_equals_sample_then_step(torch_gpu, n_board, E):
+    """oth_sample_step (one launch: k_masked's sampler + OthelloBaseEnv.step)
+    is bit-identical to sample_actions followed by step: actions, log-probs,
+    entropies, rewards, dones, the boards and the W/D/L tally, over several
+    plies with Philox draws, caller uniforms, the mode and the unmasked
+    entropy, ragged E included."""
+    torch = torch_gpu
+    from gymothelloenv_amd import VecOthelloEnv
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(n_board)
+    kw = dict(board_size=n_board, auto_reset=True, initial_rand_steps=4, seed=3, device=dev)
+    fused, split = VecOthelloEnv(E, **kw), VecOthelloEnv(E, **kw)
+    fused.reset()
+    split.reset()
+    for k in range(12):
+        logits = torch.randn(E, n_board * n_board, device=dev, generator=g) * 3
+        uni = torch.rand(E, device=dev, generator=g) if k % 3 == 1 else None
+        det, full = k % 4 == 2, k % 5 == 3
+        a1, lp1, en1, r1, d1 = fused.sample_step(logits, deterministic=det, uniforms=uni, full_entropy=full)
+        if full:
+            a2, _, _ = split.sample_actions(logits, deterministic=det, uniforms=uni)
+            from gymothelloenv_amd import masked_log_prob
+            lp2, en2 = masked_log_prob(logits, split.legal_mask(), a2, n_board, full_entropy=True)
+        else:
+            a2, lp2, en2 = split.sample_actions(logits, deterministic=det, uniforms=uni)
+        _, r2, d2, _ = split.step(a2, observe=False)
+        assert torch.equal(a1, a2), k
+        assert torch.equal(lp1, lp2) and torch.equal(en1, en2), k  # bit-identical floats
+        assert torch.equal(r1, r2) and torch.equal(d1, d2), k
+        for x, y in zip(fused.get_state(), split.get_state()):
+            assert torch.equal(x, y), k
+    assert torch.equal(fused.counts(), split.counts())
+    assert fused.ply_counter == split.ply_counter and fused.sample_counter == split.sample_counter
+
+
+def test_sample_step_graph_region_replays(torch_gpu):
+    """The fused ply captured in a HIP graph inside graph_region: replay r
+    equals the same fused plies run eagerly at the region's counters."""
+    torch = torch_gpu
+    from gymothelloenv_amd import VecOthelloEnv
+    E, n, K = 4096, 8, 6
+    dev = torch.device("cuda", 0)
+    logits = torch.randn(E, n * n, device=dev, generator=torch.Generator(device=dev).manual_seed(5))
+    kw = dict(board_size=n, auto_reset=True, initial_rand_steps=2, seed=8, device=dev)
+    eager, graphed = VecOthelloEnv(E, **kw), VecOthelloEnv(E, **kw)
+    eager.reset()
+    graphed.reset()
+    out_g = torch.empty(K, E, dtype=torch.int32, device=dev)
+    out_e = torch.empty_like(out_g)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph), graphed.graph_region() as slot:
+        for k in range(K):
+            out_g[k].copy_(graphed.sample_step(logits, log_probs=False, entropy=False)[0])
+    torch.cuda.synchronize()
+    for r in range(3):
+        eager.ply_counter = eager.sample_counter = graphed.graph_counter_base(slot) + r * K
+        for k in range(K):
+            out_e[k].copy_(eager.sample_step(logits, log_probs=False, entropy=False)[0])
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out_g, out_e)
+        for x, y in zip(graphed.get_state(), eager.get_state()):
+            assert torch.equal(x, y)

@@ -549,3 +549,52 @@ def test_observation_kernels_every_layout_and_alignment(torch_cuda, n):
             off = buf[1:].view(want.shape)  # base one element past the vector alignment
             env.observe(layout, dt, out=off)
             np.testing.assert_array_equal(off.cpu().numpy(), want, err_msg="unaligned %s %s" % (layout, dt))
+
+
+@pytest.mark.parametrize("n,opp", [(8, "random"), (6, "greedy")])
+def test_protagonist_tally_matches_oracle_rewards(torch_cuda, n, opp):
+    """counts_vs: {protagonist wins, draws, losses} of games step_vs finished,
+    with mixed protagonist colours, equals run.py:100-130's count from the
+    protagonist's final rewards (sign) replayed by the oracle."""
+    torch = torch_cuda
+    E, calls = 2048, 40
+    env = make_env(torch, E, n, auto=True, seed=17, init_rand=2)
+    prot = np.where(np.arange(E) % 3 == 0, 1, -1).astype(np.int8)
+    pid = 0 if opp == "random" else 1
+    env.reset_vs(opp, protagonist=torch.from_numpy(prot).cuda())
+    s = oracle.reset_vs(n, E, flags_of(True, False, True), pid, 0, seed=17, initial_rand_steps=2, prot=prot)
+    rng = np.random.RandomState(1)
+    tally = np.zeros(3, dtype=np.int64)
+    env.counts_vs(reset=True)
+    for c in range(1, calls + 1):
+        legal = s.legal[:, 0]
+        acts = np.array([np.flatnonzero([(int(x) >> b) & 1 for b in range(n * n)])[0] if x else 0
+                         for x in legal], dtype=np.int32)
+        acts[rng.rand(E) < 0.05] = rng.randint(0, n * n)  # a few invalid moves: sudden-death losses
+        _, r, d, _ = env.step_vs(torch.from_numpy(acts).cuda(), opponent=opp, observe=False)
+        orw, od, _ = oracle.step_vs(s, flags_of(True, False, True), pid, c, acts, seed=17, initial_rand_steps=2,
+                                    prot=prot)
+        np.testing.assert_array_equal(r.cpu().numpy(), orw)
+        np.testing.assert_array_equal(d.cpu().numpy(), od)
+        fin = od.astype(bool)
+        tally += [(orw[fin] > 0).sum(), (orw[fin] == 0).sum(), (orw[fin] < 0).sum()]
+    np.testing.assert_array_equal(env.counts_vs().cpu().numpy(), tally)
+    assert tally.sum() > 0 and tally[0] > 0 and tally[2] > 0
+
+
+def test_greedy_vs_random_split_near_readme(torch_cuda):
+    """Statistical sanity only (not a pin): greedy protagonist (black) against
+    the random opponent over 65,536 device games lands near the README's
+    61 / 5 / 34 row (README.md:46, 100 games there, so +-12 points)."""
+    torch = torch_cuda
+    E = 65536
+    env = make_env(torch, E, 8, auto=True, seed=23)
+    env.reset_vs("random", protagonist=-1)
+    env.counts_vs(reset=True)
+    for _ in range(200):
+        acts = env.greedy_actions()
+        env.step_vs(acts, opponent="random", observe=False)
+    w, d, l = env.counts_vs().cpu().numpy().astype(float)
+    tot = w + d + l
+    assert tot > E
+    assert abs(100 * w / tot - 61) < 12 and abs(100 * d / tot - 5) < 5 and abs(100 * l / tot - 34) < 12, (w, d, l)

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--device-draws", action="store_true",
                     help="Philox sampling on the device (no caller uniforms), captured inside env.graph_region()")
+    ap.add_argument("--fused", action="store_true", help="one oth_sample_step launch per ply instead of two calls")
     ap.add_argument("--lib", default=None, help="a variant build (gymothelloenv_amd/variants/liboth_<lib>.so)")
     a = ap.parse_args()
     import torch
@@ -40,9 +41,12 @@ def main():
 
     def plies(env):
         for k in range(K):
-            act, _, _ = env.sample_actions(logits, uniforms=None if a.device_draws else u[k], log_probs=False,
-                                           entropy=False)
-            env.step(act, rewards=rew, dones=don, observe=False)
+            uk = None if a.device_draws else u[k]
+            if a.fused:
+                env.sample_step(logits, uniforms=uk, log_probs=False, entropy=False, rewards=rew, dones=don)
+            else:
+                act, _, _ = env.sample_actions(logits, uniforms=uk, log_probs=False, entropy=False)
+                env.step(act, rewards=rew, dones=don, observe=False)
 
     def timed(fn):
         fn()
@@ -64,7 +68,9 @@ def main():
     with torch.cuda.graph(graph), (graphed.graph_region() if a.device_draws else contextlib.nullcontext()):
         plies(graphed)
     us_graph = timed(graph.replay)
-    print(json.dumps({"path": "sample_actions(%s) + step" % ("device Philox, graph_region" if a.device_draws else "uniforms"), "lib": a.lib, "E": E, "board_size": n, "plies_per_graph": K,
+    draws = "device Philox, graph_region" if a.device_draws else "uniforms"
+    path = ("sample_step(%s) [one launch]" if a.fused else "sample_actions(%s) + step") % draws
+    print(json.dumps({"path": path, "lib": a.lib, "E": E, "board_size": n, "plies_per_graph": K,
                       "us_per_ply_eager": us_eager, "us_per_ply_graph": us_graph,
                       "env_steps_per_s_eager": E / (us_eager * 1e-6), "env_steps_per_s_graph": E / (us_graph * 1e-6)}))
 
