@@ -78,6 +78,9 @@ using namespace oth;
 #ifndef OTH_FLIP_AND3
 #define OTH_FLIP_AND3 1  // Fills::flip toward higher squares as one 3-input AND (v_bitop3_b32) per dword
 #endif
+#ifndef OTH_RAND_PIPE
+#define OTH_RAND_PIPE 1  // k_play_rand: the next Philox block computed inside the current 4-ply group
+#endif
 #ifndef OTH_SS_STAGE
 #define OTH_SS_STAGE 0  // 1: k_sample_step stages the wave's logits rows through LDS (coalesced loads; measured slower: 8.6 -> 11.1 us per ply at 8x8)
 #endif
@@ -1131,6 +1134,34 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
         };
         if (!slow) {
             int p = 0;
+#if OTH_RAND_PIPE
+            // Philox block g/4 serves plies 4k..4k+3 (g uniform: scalar branches).
+            // The next block is computed in the current group's first ply, where
+            // its independent VALU work fills the wait for the ray-table loads.
+            while (p < plies && ((ply0 + (uint64_t)p) & 3) != 0) {
+                const uint64_t g = ply0 + (uint64_t)p;
+                ply(p, pick4(philox4(rng.seed, id, g >> 2, RNG_ACTION), (uint32_t)(g & 3)));
+                ++p;
+            }
+            if (p + 4 <= plies) {
+                U4 cur = philox4(rng.seed, id, (ply0 + (uint64_t)p) >> 2, RNG_ACTION);
+                while (p + 4 <= plies) {
+                    const U4 nxt = p + 8 <= plies ? philox4(rng.seed, id, ((ply0 + (uint64_t)p) >> 2) + 1, RNG_ACTION)
+                                                  : cur;
+                    ply(p, cur.x);
+                    ply(p + 1, cur.y);
+                    ply(p + 2, cur.z);
+                    ply(p + 3, cur.w);
+                    cur = nxt;
+                    p += 4;
+                }
+            }
+            while (p < plies) {
+                const uint64_t g = ply0 + (uint64_t)p;
+                ply(p, pick4(philox4(rng.seed, id, g >> 2, RNG_ACTION), (uint32_t)(g & 3)));
+                ++p;
+            }
+#else
             while (p < plies) {  // Philox block g/4 serves plies 4k..4k+3 (g uniform: scalar branches)
                 const uint64_t g = ply0 + (uint64_t)p;
                 const U4 d4 = philox4(rng.seed, id, g >> 2, RNG_ACTION);
@@ -1145,6 +1176,7 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
                     ++p;
                 }
             }
+#endif
             const bool tw = (mt & M_TURN_WHITE) != 0;
             s.white.w[0] = tw ? M : O;
             s.black.w[0] = tw ? O : M;
