@@ -85,7 +85,7 @@ using namespace oth;
 #define OTH_SS_STAGE 0  // 1: k_sample_step stages the wave's logits rows through LDS (coalesced loads; measured slower: 8.6 -> 11.1 us per ply at 8x8)
 #endif
 #ifndef OTH_FLIP_TURN
-#define OTH_FLIP_TURN 0  // 1: Fills::flip toward lower squares on the board turned by 180 degrees (no 64-bit clz; measured -1.5 % at 8x8, -3 % at 6x6)
+#define OTH_FLIP_TURN 2  // Fills::flip toward lower squares on the board turned by 180 degrees, no 64-bit clz (2: turned rays tabled under the unturned square, +3 % at 8x8; 1: addressed at NN-1-a, -1.5 %)
 #endif
 #ifndef OTH_DRAW_UNROLL
 #define OTH_DRAW_UNROLL 1  // k_play random: four plies unrolled per Philox block (no per-ply word rotation)
@@ -210,7 +210,10 @@ struct Solo {
 static __device__ __constant__ const int RAY_DR[8] = {0, 1, 1, 1, 0, -1, -1, -1};
 static __device__ __constant__ const int RAY_DC[8] = {1, 0, 1, -1, -1, 0, -1, 1};
 
-template <int N>
+// TURNED: the tables of the directions toward lower squares (d >= 4) hold
+// their rays on the board turned by 180 degrees (square s -> N*N-1-s), still
+// indexed by the unturned square (Fills with OTH_FLIP_TURN == 2).
+template <int N, bool TURNED = false>
 __device__ __forceinline__ void fill_rays(uint64_t* rays) {
     for (int i = threadIdx.x; i < 8 * 64; i += BLOCK) {
         const int d = i >> 6, sq = i & 63;
@@ -219,7 +222,8 @@ __device__ __forceinline__ void fill_rays(uint64_t* rays) {
             const int dr = RAY_DR[d], dc = RAY_DC[d];
             int row = sq / N + dr, col = sq % N + dc;
             while (row >= 0 && row < N && col >= 0 && col < N) {
-                r |= 1ull << (row * N + col);
+                const int s2 = row * N + col;
+                r |= 1ull << ((TURNED && d >= 4) ? N * N - 1 - s2 : s2);
                 row += dr;
                 col += dc;
             }
@@ -358,14 +362,16 @@ struct Fills {
         }
 #if OTH_FLIP_TURN
         // toward lower squares on the board turned by 180 degrees (square s ->
-        // NN-1-s, OneWord::turn180): ray d from a becomes ray d-4 from NN-1-a,
-        // toward higher squares, so the same lowest-bit form applies to the
-        // turned fill; one turn of the or-ed runs at the end
-        const uint64_t* rt = rays + (N * N - 1 - a);
+        // NN-1-s, OneWord::turn180): the ray runs toward higher squares there,
+        // so the same lowest-bit form applies to the turned fill; one turn of
+        // the or-ed runs at the end.  OTH_FLIP_TURN 2: the turned rays are
+        // tabled under the unturned square (same address as the other four);
+        // 1: ray d from a is ray d-4 from NN-1-a
+        const uint64_t* rt = OTH_FLIP_TURN == 2 ? r : rays + (N * N - 1 - a) - 4 * 64;
         uint64_t g = 0;
 #pragma unroll
         for (int d = 4; d < 8; ++d) {
-            const uint64_t ray = rt[64 * (d - 4)];
+            const uint64_t ray = rt[64 * d];
             const uint64_t tt = OneWord<N>::turn180(t[d]);
             const uint64_t y = ray & ~tt;
             g |= and3_64(ray, tt, y - 1ull);
@@ -430,6 +436,12 @@ struct FillsW {
         __syncthreads();
     }
 };
+
+// does the engine read the ray tables of the directions toward lower squares turned?
+template <typename Eng>
+struct turned_rays : std::false_type {};
+template <int N>
+struct turned_rays<Fills<N>> : std::integral_constant<bool, OTH_FLIP_TURN == 2> {};
 
 template <typename Eng>
 struct is_fills_w : std::false_type {};
@@ -906,7 +918,7 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
     ply0 += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
     __shared__ __attribute__((aligned(16))) uint64_t lds_rays[Eng::RAY_WORDS > 0 ? Eng::RAY_WORDS : 1];
     if constexpr (is_fills_w<Eng>::value) Eng::fill(lds_rays);
-    else if constexpr (Eng::RAY_WORDS > 0) fill_rays<N>(lds_rays);
+    else if constexpr (Eng::RAY_WORDS > 0) fill_rays<N, turned_rays<Eng>::value>(lds_rays);
     const int gt = blockIdx.x * BLOCK + threadIdx.x;
     const int e = gt / Eng::LANES;
     const Eng eng(gt % Eng::LANES, lds_rays);
@@ -1102,7 +1114,7 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
     static_assert(Geo<N>::W == 1, "one-word boards");
     ply0 += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
     __shared__ __attribute__((aligned(16))) uint64_t lds_rays[Fills<N>::RAY_WORDS];
-    fill_rays<N>(lds_rays);
+    fill_rays<N, turned_rays<Fills<N>>::value>(lds_rays);
     const int e = blockIdx.x * BLOCK + threadIdx.x;
     uint32_t cb = 0, cd = 0, cw = 0;
     if (e < E) {
