@@ -78,6 +78,9 @@ using namespace oth;
 #ifndef OTH_FLIP_AND3
 #define OTH_FLIP_AND3 1  // Fills::flip toward higher squares as one 3-input AND (v_bitop3_b32) per dword
 #endif
+#ifndef OTH_FAST_RANDOM_W
+#define OTH_FAST_RANDOM_W 1  // k_play_rand_w: the same restructured random play for multi-word boards (N >= 9)
+#endif
 #ifndef OTH_RAND_PIPE
 #define OTH_RAND_PIPE 1  // k_play_rand: the next Philox block computed inside the current 4-ply group
 #endif
@@ -1202,6 +1205,147 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
                     a = random_action<N>(s, action_draw(rng.seed, id, g));
                     if ((s.meta >> M_RAND_SHIFT) > 0) s.meta -= 1u << M_RAND_SHIFT;
                     step_lane<N, Fills<N>, true>(s, a, flags, r, d, win, eng);
+                    if (d) {
+                        cb += win == BLACK_DISK;
+                        cd += win == NO_DISK;
+                        cw += win == WHITE_DISK;
+                        reset_lane<N>(s, rng.seed, id, g, RNG_OPENING_AUTO, rng.init_rand);
+                        eng.prime(s);
+                    }
+                }
+                act_p[(size_t)p * E] = a;
+                rew_p[(size_t)p * E] = r;
+                done_p[(size_t)p * E] = (uint8_t)d;
+            }
+        }
+        store_lane<N>(s, boards, meta, legal, e);
+    }
+    tally(wdl, cb, cd, cw);
+}
+
+// play_rand_fast for multi-word boards (N >= 9, the FillsW engine): the same
+// (mover, opponent) form with BB<W> words; every multi-word select is word by
+// word (a selected member address puts the lane in scratch).
+template <int N>
+__device__ __forceinline__ void play_rand_fast_w(BB<Geo<N>::W>& M, BB<Geo<N>::W>& O, BB<Geo<N>::W>& L,
+                                                 uint32_t& meta, const FillsW<N>& eng, uint32_t u, uint32_t flags,
+                                                 const Rng& rng, uint32_t id, uint64_t g, int& a, int& r, int& d,
+                                                 uint32_t& cb, uint32_t& cd, uint32_t& cw) {
+    constexpr int W = Geo<N>::W;
+    constexpr int NN = N * N;
+    a = select_bit(L, scale_index(u, popcount(L)));  // RandomPolicy (simple_policies.py:37-41); L != 0
+    meta -= (meta & 0xff00u) ? (1u << M_RAND_SHIFT) : 0u;
+    const BB<W> m = square<W>(a);
+    const BB<W> f = eng.flip(M, O, a);  // update_board (othello.py:391-410)
+    const BB<W> Mn = M | f | m, On = O & ~f;
+    const bool full = !any(~(Mn | On) & Geo<N>::BOARD);  // :425-426
+    BB<W> Ln = eng.legal(On, Mn);                          // the opponent's possible_moves (:436)
+    const bool pass = !any(Ln) && !full;
+    if (pass) Ln = eng.legal(Mn, On);  // :437-440
+    const bool term = full || !any(Ln);
+    const bool swap = !pass && !full;
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+        M.w[i] = swap ? On.w[i] : Mn.w[i];
+        O.w[i] = swap ? Mn.w[i] : On.w[i];
+    }
+    L = Ln;
+    meta ^= swap ? M_TURN_WHITE : 0u;
+    r = 0;
+    d = term ? 1 : 0;
+    if (term) {
+        const bool tw = (meta & M_TURN_WHITE) != 0;
+        const int pc = popcount(Mn), oc = popcount(On);
+        if (flags & OTH_DISK_REWARD) r = oc == 0 ? NN : pc - oc;  // :446-459
+        else r = pc > oc ? 1 : (pc < oc ? -1 : 0);
+        const bool mover_wins = pc > oc, opp_wins = pc < oc;
+        cb += tw ? opp_wins : mover_wins;
+        cd += !mover_wins && !opp_wins;
+        cw += tw ? mover_wins : opp_wins;
+        M = Start<N>::BLACK;  // auto-reset (othello.py:256-271)
+        O = Start<N>::WHITE;
+        L = eng.legal(M, O);
+        uint32_t rl = 0;
+        if (rng.init_rand > 0)
+            rl = (uint32_t)scale_index(philox_x(rng.seed, id, g, RNG_OPENING_AUTO), rng.init_rand / 2 + 1) * 2u;
+        meta = (rl & 0xffu) << M_RAND_SHIFT;
+    }
+}
+
+// k_play_rand for multi-word boards (config 5's 10x10 and every N >= 9).
+template <int N>
+__global__ __launch_bounds__(BLOCK) void k_play_rand_w(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
+                                                       uint64_t* __restrict__ legal, int E, uint32_t flags, int plies,
+                                                       int32_t* __restrict__ actions, int32_t* __restrict__ rewards,
+                                                       uint8_t* __restrict__ dones,
+                                                       unsigned long long* __restrict__ wdl, Rng rng, uint64_t ply0) {
+    constexpr int W = Geo<N>::W;
+    static_assert(W > 1, "multi-word boards");
+    ply0 += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
+    __shared__ __attribute__((aligned(16))) uint64_t lds_rays[FillsW<N>::RAY_WORDS];
+    FillsW<N>::fill(lds_rays);
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    uint32_t cb = 0, cd = 0, cw = 0;
+    if (e < E) {
+        const uint32_t id = rng.id_base + (uint32_t)e;
+        const FillsW<N> eng(0, lds_rays);
+        Lane<N> s;
+        load_lane<N>(s, boards, meta, legal, e);
+        const bool tw0 = (s.meta & M_TURN_WHITE) != 0;
+        BB<W> M, O, L = s.legal;
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+            M.w[i] = tw0 ? s.white.w[i] : s.black.w[i];
+            O.w[i] = tw0 ? s.black.w[i] : s.white.w[i];
+        }
+        uint32_t mt = s.meta & (0xff00u | M_TURN_WHITE);
+        eng.prime(s);
+        const bool slow = __any((s.meta & M_TERMINATED) != 0);
+        int32_t* act_p = actions + e;
+        int32_t* rew_p = rewards + e;
+        uint8_t* done_p = dones + e;
+        auto ply = [&](uint64_t g, uint32_t u) __attribute__((always_inline)) {
+            int a, r, d;
+            play_rand_fast_w<N>(M, O, L, mt, eng, u, flags, rng, id, g, a, r, d, cb, cd, cw);
+            *act_p = a;
+            *rew_p = r;
+            *done_p = (uint8_t)d;
+            act_p += E;
+            rew_p += E;
+            done_p += E;
+        };
+        if (!slow) {
+            int p = 0;
+            while (p < plies) {  // Philox block g/4 serves plies 4k..4k+3 (g uniform: scalar branches)
+                const uint64_t g = ply0 + (uint64_t)p;
+                const U4 d4 = philox4(rng.seed, id, g >> 2, RNG_ACTION);
+                if ((g & 3) == 0 && p + 4 <= plies) {
+                    ply(g, d4.x);
+                    ply(g + 1, d4.y);
+                    ply(g + 2, d4.z);
+                    ply(g + 3, d4.w);
+                    p += 4;
+                } else {
+                    ply(g, pick4(d4, (uint32_t)(g & 3)));
+                    ++p;
+                }
+            }
+            const bool tw = (mt & M_TURN_WHITE) != 0;
+#pragma unroll
+            for (int i = 0; i < W; ++i) {
+                s.white.w[i] = tw ? M.w[i] : O.w[i];
+                s.black.w[i] = tw ? O.w[i] : M.w[i];
+            }
+            s.legal = L;
+            s.meta = mt;
+        } else {
+            for (int p = 0; p < plies; ++p) {
+                const uint64_t g = ply0 + (uint64_t)p;
+                int a = -1, r = 0, d = 1, win = NO_DISK;
+                if (!(s.meta & M_TERMINATED)) {
+                    a = random_action<N>(s, action_draw(rng.seed, id, g));
+                    if ((s.meta >> M_RAND_SHIFT) > 0) s.meta -= 1u << M_RAND_SHIFT;
+                    step_lane<N, FillsW<N>, true>(s, a, flags, r, d, win, eng);
                     if (d) {
                         cb += win == BLACK_DISK;
                         cd += win == NO_DISK;

@@ -167,9 +167,9 @@ def test_fills_engine_flag_combinations(torch_cuda, n, policy, sd, dr, auto, ini
     np.testing.assert_array_equal(env.counts().cpu().numpy(), owdl)
 
 
-@pytest.mark.parametrize("n", [6, 8])
+@pytest.mark.parametrize("n", [6, 8, 10, 13])
 def test_random_rollout_with_boards_loaded_terminated(torch_cuda, n):
-    """k_play_rand's fallback: waves holding a board that was loaded
+    """k_play_rand's (and k_play_rand_w's) fallback: waves holding a board that was loaded
     terminated (set_state) run the generic ply loop; that board reports
     action -1 / done 1 every ply and is never reset (oth_step_policy's
     semantics), every other board of the wave plays on.  Equal to the oracle."""
