@@ -78,6 +78,9 @@ using namespace oth;
 #ifndef OTH_FLIP_AND3
 #define OTH_FLIP_AND3 1  // Fills::flip toward higher squares as one 3-input AND (v_bitop3_b32) per dword
 #endif
+#ifndef OTH_FAST_GREEDY
+#define OTH_FAST_GREEDY 1  // k_play_rand<N, GREEDY>: the same restructuring for greedy play (N <= 8)
+#endif
 #ifndef OTH_FAST_RANDOM_W
 #define OTH_FAST_RANDOM_W 1  // k_play_rand_w: the same restructured random play for multi-word boards (N >= 9)
 #endif
@@ -1052,14 +1055,22 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
 //   * the opponent's legal scan runs unconditionally (on a full board it
 //     finds nothing: no empty square); only a pass re-scans, in place.
 // The random pick is always legal, so sudden death never triggers here.
-template <int N>
+// POLICY GREEDY (k_play_rand<N, GREEDY>): GreedyPolicy's move from the bit
+// planes of the carried fills (simple_policies.py:69-92), a random move while
+// random-opening plies remain (SimpleOthelloEnv, othello.py:60-79).
+template <int N, int POLICY = OTH_POLICY_RANDOM>
 __device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_t& L, uint32_t& meta,
                                                const Fills<N>& eng, uint32_t u, uint32_t flags, const Rng& rng,
                                                uint32_t id, uint64_t g, int& a, int& r, int& d, uint32_t& cb,
                                                uint32_t& cd, uint32_t& cw) {
     constexpr uint64_t BD = Geo<N>::BOARD.w[0];
     constexpr int NN = N * N;
-    a = select64(L, scale_index(u, popc64(L)));  // RandomPolicy (simple_policies.py:37-41); L != 0
+    if constexpr (POLICY == OTH_POLICY_RANDOM) {
+        a = select64(L, scale_index(u, popc64(L)));  // RandomPolicy (simple_policies.py:37-41); L != 0
+    } else {
+        if (meta & 0xff00u) a = select64(L, scale_index(action_draw(rng.seed, id, g), popc64(L)));
+        else a = OneWord<N>::greedy(eng.t, L);
+    }
     meta -= (meta & 0xff00u) ? (1u << M_RAND_SHIFT) : 0u;  // a random-opening ply used up
     const uint64_t m = 1ull << a;
     BB<1> dummy;
@@ -1108,7 +1119,7 @@ __device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_
     }
 }
 
-template <int N>
+template <int N, int POLICY = OTH_POLICY_RANDOM>
 __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
                                                      uint64_t* __restrict__ legal, int E, uint32_t flags, int plies,
                                                      int32_t* __restrict__ actions, int32_t* __restrict__ rewards,
@@ -1139,7 +1150,7 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
         uint8_t* done_p = dones + e;
         auto ply = [&](int p, uint32_t u) __attribute__((always_inline)) {
             int a, r, d;
-            play_rand_fast<N>(M, O, L, mt, eng, u, flags, rng, id, ply0 + (uint64_t)p, a, r, d, cb, cd, cw);
+            play_rand_fast<N, POLICY>(M, O, L, mt, eng, u, flags, rng, id, ply0 + (uint64_t)p, a, r, d, cb, cd, cw);
             *act_p = a;
             *rew_p = r;
             *done_p = (uint8_t)d;
@@ -1147,7 +1158,10 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
             rew_p += E;
             done_p += E;
         };
-        if (!slow) {
+        if (!slow && POLICY != OTH_POLICY_RANDOM) {  // scripted policy: draws only on opening plies
+            for (int p = 0; p < plies; ++p) ply(p, 0u);
+        }
+        if (!slow && POLICY == OTH_POLICY_RANDOM) {
             int p = 0;
 #if OTH_RAND_PIPE
             // Philox block g/4 serves plies 4k..4k+3 (g uniform: scalar branches).
@@ -1192,6 +1206,8 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
                 }
             }
 #endif
+        }
+        if (!slow) {
             const bool tw = (mt & M_TURN_WHITE) != 0;
             s.white.w[0] = tw ? M : O;
             s.black.w[0] = tw ? O : M;
@@ -1202,7 +1218,10 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
                 const uint64_t g = ply0 + (uint64_t)p;
                 int a = -1, r = 0, d = 1, win = NO_DISK;
                 if (!(s.meta & M_TERMINATED)) {
-                    a = random_action<N>(s, action_draw(rng.seed, id, g));
+                    if (POLICY == OTH_POLICY_RANDOM || (s.meta >> M_RAND_SHIFT) > 0)
+                        a = random_action<N>(s, action_draw(rng.seed, id, g));
+                    else
+                        a = policy_action<N, POLICY>(s, eng);
                     if ((s.meta >> M_RAND_SHIFT) > 0) s.meta -= 1u << M_RAND_SHIFT;
                     step_lane<N, Fills<N>, true>(s, a, flags, r, d, win, eng);
                     if (d) {

@@ -63,6 +63,14 @@ void launch_k_play(int lanes_per_board, oth_env* env, int n_plies, int32_t* acti
             return;
         }
     }
+    if constexpr (OTH_FAST_GREEDY && POL == OTH_POLICY_GREEDY && std::is_same<Eng, Fills<N>>::value) {
+        if (actions && rewards && dones && (env->flags & OTH_AUTO_RESET)) {
+            hipLaunchKernelGGL((k_play_rand<N, OTH_POLICY_GREEDY>), grid, block, 0, st, env->boards, env->meta,
+                               env->legal, env->E, env->flags, n_plies, actions, rewards, dones, env->wdl,
+                               rng_of(env), ply0);
+            return;
+        }
+    }
     if constexpr (OTH_FAST_RANDOM_W && POL == OTH_POLICY_RANDOM && std::is_same<Eng, FillsW<N>>::value) {
         if (actions && rewards && dones && (env->flags & OTH_AUTO_RESET)) {
             hipLaunchKernelGGL((k_play_rand_w<N>), grid, block, 0, st, env->boards, env->meta, env->legal, env->E,
