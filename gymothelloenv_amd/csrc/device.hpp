@@ -78,6 +78,9 @@ using namespace oth;
 #ifndef OTH_FLIP_AND3
 #define OTH_FLIP_AND3 1  // Fills::flip toward higher squares as one 3-input AND (v_bitop3_b32) per dword
 #endif
+#ifndef OTH_OPEN_SPLIT
+#define OTH_OPEN_SPLIT 1  // k_play_rand: a copy of the ply loop without random-opening bookkeeping
+#endif
 #ifndef OTH_FAST_GREEDY
 #define OTH_FAST_GREEDY 1  // k_play_rand<N, GREEDY>: the same restructuring for greedy play (N <= 8)
 #endif
@@ -1058,7 +1061,10 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
 // POLICY GREEDY (k_play_rand<N, GREEDY>): GreedyPolicy's move from the bit
 // planes of the carried fills (simple_policies.py:69-92), a random move while
 // random-opening plies remain (SimpleOthelloEnv, othello.py:60-79).
-template <int N, int POLICY = OTH_POLICY_RANDOM>
+// OPEN: some board of the wave may have random-opening plies left (the
+// handle's initial_rand_steps > 0, or a board loaded with some); without, the
+// opening bookkeeping is compiled out.
+template <int N, int POLICY = OTH_POLICY_RANDOM, bool OPEN = true>
 __device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_t& L, uint32_t& meta,
                                                const Fills<N>& eng, uint32_t u, uint32_t flags, const Rng& rng,
                                                uint32_t id, uint64_t g, int& a, int& r, int& d, uint32_t& cb,
@@ -1067,11 +1073,13 @@ __device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_
     constexpr int NN = N * N;
     if constexpr (POLICY == OTH_POLICY_RANDOM) {
         a = select64(L, scale_index(u, popc64(L)));  // RandomPolicy (simple_policies.py:37-41); L != 0
-    } else {
+    } else if constexpr (OPEN) {
         if (meta & 0xff00u) a = select64(L, scale_index(action_draw(rng.seed, id, g), popc64(L)));
         else a = OneWord<N>::greedy(eng.t, L);
+    } else {
+        a = OneWord<N>::greedy(eng.t, L);
     }
-    meta -= (meta & 0xff00u) ? (1u << M_RAND_SHIFT) : 0u;  // a random-opening ply used up
+    if constexpr (OPEN) meta -= (meta & 0xff00u) ? (1u << M_RAND_SHIFT) : 0u;  // a random-opening ply used up
     const uint64_t m = 1ull << a;
     BB<1> dummy;
     dummy.w[0] = 0;
@@ -1148,9 +1156,12 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
         int32_t* act_p = actions + e;
         int32_t* rew_p = rewards + e;
         uint8_t* done_p = dones + e;
+        auto fast = [&](auto OPENC) __attribute__((always_inline)) {
+        constexpr bool OPEN = decltype(OPENC)::value;
         auto ply = [&](int p, uint32_t u) __attribute__((always_inline)) {
             int a, r, d;
-            play_rand_fast<N, POLICY>(M, O, L, mt, eng, u, flags, rng, id, ply0 + (uint64_t)p, a, r, d, cb, cd, cw);
+            play_rand_fast<N, POLICY, OPEN>(M, O, L, mt, eng, u, flags, rng, id, ply0 + (uint64_t)p, a, r, d, cb, cd,
+                                            cw);
             *act_p = a;
             *rew_p = r;
             *done_p = (uint8_t)d;
@@ -1158,11 +1169,11 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
             rew_p += E;
             done_p += E;
         };
-        if (!slow && POLICY != OTH_POLICY_RANDOM) {  // scripted policy: draws only on opening plies
+        if (POLICY != OTH_POLICY_RANDOM) {  // scripted policy: draws only on opening plies
             for (int p = 0; p < plies; ++p) ply(p, 0u);
+            return;
         }
-        if (!slow && POLICY == OTH_POLICY_RANDOM) {
-            int p = 0;
+        int p = 0;
 #if OTH_RAND_PIPE
             // Philox block g/4 serves plies 4k..4k+3 (g uniform: scalar branches).
             // The next block is computed in the current group's first ply, where
@@ -1206,8 +1217,11 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
                 }
             }
 #endif
-        }
+        };
         if (!slow) {
+            // no opening bookkeeping when no board of the wave can have opening plies
+            if (OTH_OPEN_SPLIT && rng.init_rand == 0 && !__any((mt & 0xff00u) != 0)) fast(std::false_type{});
+            else fast(std::true_type{});
             const bool tw = (mt & M_TURN_WHITE) != 0;
             s.white.w[0] = tw ? M : O;
             s.black.w[0] = tw ? O : M;
