@@ -93,6 +93,21 @@ using namespace oth;
 #ifndef OTH_SS_STAGE
 #define OTH_SS_STAGE 0  // 1: k_sample_step stages the wave's logits rows through LDS (coalesced loads; measured slower: 8.6 -> 11.1 us per ply at 8x8)
 #endif
+#ifndef OTH_SS_PAIR
+#define OTH_SS_PAIR 1  // oth_sample_step on lane pairs for one-word boards (k_sample_step2)
+#endif
+#ifndef OTH_SS_QUAD
+#define OTH_SS_QUAD 1  // oth_sample_step on lane quads for one-word boards (k_sample_step4) up to OTH_SS_QUAD_MAX_E
+#endif
+#ifndef OTH_SS_QUAD_MAX_E
+#define OTH_SS_QUAD_MAX_E 16384  // boards: 4 lanes each fill at most 1,024 waves (one per SIMD)
+#endif
+#ifndef OTH_SS2_STAGE
+#define OTH_SS2_STAGE 1  // k_sample_step2 (8x8): the wave's logits rows through LDS, coalesced loads
+#endif
+#ifndef OTH_SS_ABL
+#define OTH_SS_ABL 0
+#endif
 #ifndef OTH_FLIP_TURN
 #define OTH_FLIP_TURN 2  // Fills::flip toward lower squares on the board turned by 180 degrees, no 64-bit clz (2: turned rays tabled under the unturned square, +3 % at 8x8; 1: addressed at NN-1-a, -1.5 %)
 #endif
@@ -216,19 +231,21 @@ struct Solo {
 // Ray tables for one-word boards: rays[d*64 + sq] = the squares strictly beyond
 // sq in direction d, up to the edge.  d 0..3 point to higher squares (E, S, SE,
 // SW), d 4..7 to lower ones (W, N, NW, NE).  Built in LDS once per launch.
-static __device__ __constant__ const int RAY_DR[8] = {0, 1, 1, 1, 0, -1, -1, -1};
-static __device__ __constant__ const int RAY_DC[8] = {1, 0, 1, -1, -1, 0, -1, 1};
+// Steps (row, col) of direction d: RAY_DR = {0, 1, 1, 1, 0, -1, -1, -1},
+// RAY_DC = {1, 0, 1, -1, -1, 0, -1, 1} (nibbles of the immediates in fill_rays).
 
 // TURNED: the tables of the directions toward lower squares (d >= 4) hold
 // their rays on the board turned by 180 degrees (square s -> N*N-1-s), still
 // indexed by the unturned square (Fills with OTH_FLIP_TURN == 2).
-template <int N, bool TURNED = false>
+template <int N, bool TURNED = false, bool SYNC = true>
 __device__ __forceinline__ void fill_rays(uint64_t* rays) {
     for (int i = threadIdx.x; i < 8 * 64; i += BLOCK) {
         const int d = i >> 6, sq = i & 63;
         uint64_t r = 0;
         if (sq < N * N) {
-            const int dr = RAY_DR[d], dc = RAY_DC[d];
+            // RAY_DR / RAY_DC as sign-extended nibbles: no constant-memory loads
+            const int dr = __builtin_amdgcn_sbfe((int)0xFFF01110u, 4 * d, 4);
+            const int dc = __builtin_amdgcn_sbfe((int)0x1F0FF101u, 4 * d, 4);
             int row = sq / N + dr, col = sq % N + dc;
             while (row >= 0 && row < N && col >= 0 && col < N) {
                 const int s2 = row * N + col;
@@ -239,7 +256,7 @@ __device__ __forceinline__ void fill_rays(uint64_t* rays) {
         }
         rays[i] = r;
     }
-    __syncthreads();
+    if (SYNC) __syncthreads();
 }
 
 // update_board's flips from one square (othello.py:391-410) with the ray
@@ -538,6 +555,64 @@ struct Duo {
     }
     __device__ __forceinline__ void prime(const Lane<N>&) const {}
     __device__ __forceinline__ bool leader() const { return h == 0; }
+};
+
+// Quartet<N>: four lanes per board (N <= 8, one word), lanes 4k..4k+3 of a DPP
+// quad: lane q scans one axis (E/W, S/N, SE/NW, SW/NE) and computes the flips
+// of its two ray directions (q toward higher squares, q + 4 toward lower);
+// the four parts are or-ed through quad_perm [1,0,3,2] and [2,3,0,1].  As in
+// Duo, every decision of step_lane is taken on quad-uniform values.
+template <int N>
+struct Quartet {
+    static_assert(Geo<N>::W == 1, "Quartet engine is for one-word boards (N <= 8)");
+    static constexpr int LANES = 4;
+    static constexpr int RAY_WORDS = 8 * 64;
+    static constexpr uint64_t BD = Geo<N>::BOARD.w[0], IN = Geo<N>::INNER.w[0];
+    const uint64_t* rays;  // this lane's "up" table; its "down" table is 4 * 64 words further
+    uint32_t sh;           // axis shift: 1, N, N + 1, N - 1
+    uint64_t pm;           // propagator mask: the vertical axis may pass edge columns
+    int q;
+    __device__ __forceinline__ Quartet(int lane_q, const uint64_t* lds) : q(lane_q) {
+        rays = lds + 64 * lane_q;
+        sh = lane_q == 0 ? 1u : (lane_q == 1 ? (uint32_t)N : (lane_q == 2 ? N + 1u : N - 1u));
+        pm = lane_q == 1 ? BD : IN;
+    }
+    __device__ __forceinline__ static uint32_t quad_or32(uint32_t x) {
+        x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
+        return x | (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);
+    }
+    __device__ __forceinline__ static uint64_t quad_or(uint64_t x) {
+        return ((uint64_t)quad_or32((uint32_t)(x >> 32)) << 32) | quad_or32((uint32_t)x);
+    }
+    __device__ __forceinline__ BB<1> legal(const BB<1>& Pb, const BB<1>& Ob) const {
+        const uint64_t P = Pb.w[0], O = Ob.w[0];
+        uint64_t L = 0;
+        Duo<N>::axis(P, O & pm, sh, L);
+        BB<1> r;
+        r.w[0] = quad_or(L) & ~(P | O) & BD;
+        return r;
+    }
+    __device__ __forceinline__ BB<1> flip(const BB<1>& Pb, const BB<1>& Ob, int a) const {
+        const uint64_t P = Pb.w[0], nO = ~Ob.w[0];
+        uint64_t f;
+        {  // toward higher squares: the nearest non-opponent square is the lowest set bit
+            const uint64_t ray = rays[a];
+            const uint64_t x = ray & nO;
+            const uint64_t fb = x & (0ull - x);
+            f = (fb & P) ? (ray & (fb - 1ull)) : 0ull;
+        }
+        {  // toward lower squares: the highest set bit
+            const uint64_t ray = rays[4 * 64 + a];
+            const uint64_t x = ray & nO;
+            const uint64_t hb = x ? (0x8000000000000000ull >> __clzll(x)) : 0ull;
+            f |= (hb & P) ? (ray & (0ull - (hb << 1))) : 0ull;
+        }
+        BB<1> out;
+        out.w[0] = quad_or(f);
+        return out;
+    }
+    __device__ __forceinline__ void prime(const Lane<N>&) const {}
+    __device__ __forceinline__ bool leader() const { return q == 0; }
 };
 
 // OthelloBaseEnv.reset (othello.py:265-271); rand_left = SimpleOthelloEnv's
@@ -1442,7 +1517,25 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step(uint64_t* __restrict__ bo
             __syncthreads();
             row = ws + lane * (QN + 1);
         }
+#if OTH_SS_ABL  // timing ablations (tools/ab_sample_step.py): 1 no sampling, 2 the logits loads only
+        if (mine_live) {
+            const uint64_t lw = s.legal.w[0];
+            mine.a = lw ? __builtin_ctzll(lw) : 0;
+            if (OTH_SS_ABL == 2) {
+                const float* rw = logits + (size_t)t * (size_t)ld;
+                float acc = 0.f;
+#pragma unroll
+                for (int q = 0; q < NN; q += 4) {
+                    const oth_ms::f32x4 v = *reinterpret_cast<const oth_ms::f32x4*>(rw + q);
+                    acc += (v.x + v.y) + (v.z + v.w);
+                }
+                if (acc == 12345.f) mine.a = 1;
+            }
+        }
+        if (false)
+#else
         if (mine_live)
+#endif
             mine = oth_ms::sample_lane<CH, G, VEC, FULL>((int)t, NN, logits, ld, legal, uniforms, rng.seed,
                                                          rng.id_base, counter, mode, 0, log_probs != nullptr,
                                                          entropy != nullptr, row);
@@ -1486,6 +1579,135 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step(uint64_t* __restrict__ bo
         store_lane<N>(s, boards, meta, legal, e);
         if (rewards) rewards[e] = r;
         if (dones) dones[e] = (uint8_t)d;
+    }
+    tally(wdl, cb, cd, cw);
+}
+
+// k_sample_step on lane pairs (one-word boards): the pair samples its board
+// with oth_ms::sample_pair (bit-identical to the one-lane form) and steps it
+// with the Duo engine (half the axes and rays per lane, or-ed through DPP).
+// Twice the waves of k_sample_step for the same boards, so two waves share
+// each SIMD at 65,536 boards: the loads of one hide behind the other's VALU
+// work, and the pair halves the per-lane sampling and scanning.
+template <int N, bool VEC, bool FULL>
+__global__ __launch_bounds__(BLOCK) void k_sample_step2(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
+                                                        uint64_t* __restrict__ legal, int E, uint32_t flags,
+                                                        const float* __restrict__ logits, long long ld,
+                                                        const float* __restrict__ uniforms, uint64_t counter,
+                                                        int mode, int32_t* __restrict__ actions,
+                                                        float* __restrict__ log_probs, float* __restrict__ entropy,
+                                                        int32_t* __restrict__ rewards, uint8_t* __restrict__ dones,
+                                                        unsigned long long* __restrict__ wdl, Rng rng, uint64_t ply) {
+    static_assert(Geo<N>::W == 1 && OTH_MS_G == 4, "lane pairs restate k_masked's four lanes of one-word boards");
+    constexpr int NN = N * N;
+    ply += rng.ply_off[0];      // graph-region offsets (oth_graph_end); 0 eagerly
+    counter += rng.ply_off[1];  // the sample counter's, as k_masked
+    __shared__ __attribute__((aligned(16))) uint64_t lds_rays[Duo<N>::RAY_WORDS];
+    const long long gt = (long long)blockIdx.x * BLOCK + threadIdx.x;
+    const int e = (int)(gt >> 1), h = (int)(gt & 1);
+    const Duo<N> eng(h, lds_rays);
+    uint32_t cb = 0, cd = 0, cw = 0;
+    Lane<N> s;  // the board's loads are issued first, in flight with the logits loads
+    if (e < E) load_lane<N>(s, boards, meta, legal, e);
+    auto board = [&](auto STAGEDC, const oth_ms::f32x4* staged) __attribute__((always_inline)) {
+        if (e >= E) return;  // pair-uniform: both lanes of a pair share e
+        const oth_ms::Pick pk = oth_ms::sample_pair<VEC, FULL, decltype(STAGEDC)::value>(
+            e, h, NN, logits, ld, s.legal.w[0], uniforms, rng.seed, rng.id_base, counter, mode, log_probs != nullptr,
+            entropy != nullptr, staged);
+        const bool was_term = (s.meta & M_TERMINATED) != 0;
+        int r, d, win;
+        step_lane<N>(s, pk.a, flags, r, d, win, eng);
+        if (d && !was_term) {
+            if (h == 0) {
+                cb = win == BLACK_DISK;
+                cd = win == NO_DISK;
+                cw = win == WHITE_DISK;
+            }
+            if (flags & OTH_AUTO_RESET)
+                reset_lane<N>(s, rng.seed, rng.id_base + (uint32_t)e, ply, RNG_OPENING_AUTO, rng.init_rand);
+        }
+        if (h == 0) {
+            actions[e] = pk.a;
+            if (log_probs) log_probs[e] = pk.lp;
+            if (entropy) entropy[e] = pk.ent;
+            store_lane<N>(s, boards, meta, legal, e);
+            if (rewards) rewards[e] = r;
+            if (dones) dones[e] = (uint8_t)d;
+        }
+    };
+    // the ray tables are built after the loads are issued (their latency hides the build)
+    if constexpr (VEC && N == 8 && OTH_SS2_STAGE) {  // the wave's 32 rows through LDS: coalesced loads
+        __shared__ oth_ms::f32x4 stage[(BLOCK / 64) * 32 * oth_ms::PAIR_ROW];
+        const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        oth_ms::f32x4 v[8];
+        oth_ms::load_pair_rows(v, (gt - lane) >> 1, E, logits, ld, lane);
+        fill_rays<N, false, false>(lds_rays);  // while the rows are in flight
+        const oth_ms::f32x4* rows = oth_ms::store_pair_rows(stage + wv * 32 * oth_ms::PAIR_ROW, v, lane);
+        __syncthreads();  // the ray tables (the rows need only the wave's own order)
+        board(std::true_type{}, rows);
+    } else {
+        fill_rays<N, false>(lds_rays);
+        board(std::false_type{}, nullptr);
+    }
+    tally(wdl, cb, cd, cw);
+}
+
+// k_sample_step on lane quads (one-word boards): the quad IS k_masked's group
+// of G = 4 lanes for the board (load_slot / finish_slot, the same code, so the
+// pick is k_masked's), then steps it with the Quartet engine.  Four times the
+// waves of the one-lane form: each lane's instruction stream is a quarter of
+// the sampling and of the scans, and four waves share each SIMD.
+template <int N, bool VEC, bool FULL>
+__global__ __launch_bounds__(BLOCK) void k_sample_step4(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
+                                                        uint64_t* __restrict__ legal, int E, uint32_t flags,
+                                                        const float* __restrict__ logits, long long ld,
+                                                        const float* __restrict__ uniforms, uint64_t counter,
+                                                        int mode, int32_t* __restrict__ actions,
+                                                        float* __restrict__ log_probs, float* __restrict__ entropy,
+                                                        int32_t* __restrict__ rewards, uint8_t* __restrict__ dones,
+                                                        unsigned long long* __restrict__ wdl, Rng rng, uint64_t ply) {
+    static_assert(Geo<N>::W == 1 && OTH_MS_G == 4, "lane quads are k_masked's four lanes of one-word boards");
+    constexpr int NN = N * N;
+    ply += rng.ply_off[0];      // graph-region offsets (oth_graph_end); 0 eagerly
+    counter += rng.ply_off[1];  // the sample counter's, as k_masked
+    __shared__ __attribute__((aligned(16))) uint64_t lds_rays[Quartet<N>::RAY_WORDS];
+    const long long gt = (long long)blockIdx.x * BLOCK + threadIdx.x;
+    const int e = (int)(gt >> 2), q = (int)(gt & 3);
+    const Quartet<N> eng(q, lds_rays);
+    uint32_t cb = 0, cd = 0, cw = 0;
+    Lane<N> s;  // the board's and the logits' loads are issued before the ray tables are built
+    oth_ms::Slot<1, 4> b;
+    b.e = e;
+    b.live = e < E;
+    if (e < E) {
+        load_lane<N>(s, boards, meta, legal, e);
+        oth_ms::load_slot<1, 4, VEC>(b, q, NN, logits, ld, legal);
+    }
+    fill_rays<N, false>(lds_rays);
+    if (e < E) {  // quad-uniform: the four lanes of a quad share e
+        const oth_ms::Pick pk = oth_ms::finish_slot<1, 4, FULL>(b, q, NN, logits, ld, uniforms, rng.seed, rng.id_base,
+                                                                counter, mode, 0, log_probs != nullptr,
+                                                                entropy != nullptr);
+        const bool was_term = (s.meta & M_TERMINATED) != 0;
+        int r, d, win;
+        step_lane<N>(s, pk.a, flags, r, d, win, eng);
+        if (d && !was_term) {
+            if (q == 0) {
+                cb = win == BLACK_DISK;
+                cd = win == NO_DISK;
+                cw = win == WHITE_DISK;
+            }
+            if (flags & OTH_AUTO_RESET)
+                reset_lane<N>(s, rng.seed, rng.id_base + (uint32_t)e, ply, RNG_OPENING_AUTO, rng.init_rand);
+        }
+        if (q == 0) {
+            actions[e] = pk.a;
+            if (log_probs) log_probs[e] = pk.lp;
+            if (entropy) entropy[e] = pk.ent;
+            store_lane<N>(s, boards, meta, legal, e);
+            if (rewards) rewards[e] = r;
+            if (dones) dones[e] = (uint8_t)d;
+        }
     }
     tally(wdl, cb, cd, cw);
 }

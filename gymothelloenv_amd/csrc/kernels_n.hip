@@ -122,6 +122,26 @@ template <int N, int G, bool VEC, bool FULL>
 void launch_ss(oth_env* env, const float* logits, long long ld, const float* uniforms, uint64_t counter, int mode,
                int32_t* actions, float* log_probs, float* entropy, int32_t* rewards, uint8_t* dones, uint64_t ply,
                hipStream_t st) {
+    // lane quads (k_sample_step4) while the quads fill at most one wave per SIMD: latency-bound sizes,
+    // where a quarter of the per-lane instruction stream wins (8x8, E = 3001: 5.67 -> 4.83 us per ply);
+    // beyond, the quads' duplicated step work loses to pairs (65,536: 7.02 -> 7.45)
+    // (the tally slots oth_create sizes cover the quads' grid: one slot per block)
+    if constexpr (Geo<N>::W == 1 && OTH_SS_QUAD) {
+        if (env->E <= OTH_SS_QUAD_MAX_E && grid_for(4LL * env->E) <= env->nslots) {
+            hipLaunchKernelGGL((k_sample_step4<N, VEC, FULL>), dim3(grid_for(4LL * env->E)), dim3(BLOCK), 0, st,
+                               env->boards, env->meta, env->legal, env->E, env->flags, logits, ld, uniforms, counter,
+                               mode, actions, log_probs, entropy, rewards, dones, env->wdl, rng_of(env), ply);
+            return;
+        }
+    }
+    // lane pairs (k_sample_step2) for 7x7 and 8x8: 8x8 7.77 -> 7.22 us per ply graphed (-8.5 % with
+    // log-probs); 6x6 loses (5.1 -> 6.0: the one-lane form folds the squares past N*N away)
+    if constexpr (Geo<N>::W == 1 && N >= 7 && OTH_SS_PAIR) {
+        hipLaunchKernelGGL((k_sample_step2<N, VEC, FULL>), dim3(grid_for(2LL * env->E)), dim3(BLOCK), 0, st,
+                           env->boards, env->meta, env->legal, env->E, env->flags, logits, ld, uniforms, counter, mode,
+                           actions, log_probs, entropy, rewards, dones, env->wdl, rng_of(env), ply);
+        return;
+    }
     constexpr bool ONE = OTH_SS_ONE && Geo<N>::W <= 2;
     const long long lanes = ONE ? (long long)env->E : ((long long)env->E + G - 1) / G * G;
     hipLaunchKernelGGL((k_sample_step<N, G, VEC, FULL, ONE>), dim3(grid_for(lanes)), dim3(BLOCK), 0, st, env->boards,

@@ -158,6 +158,44 @@ __device__ __forceinline__ float legal_or_ninf(uint32_t nib, int j, float x) {
     return ((nib >> j) & 1u) ? x : -INFINITY;
 #endif
 }
+// Maxima on raw v_max3_f32 / v_max_f32: fmaxf of a value the compiler cannot
+// prove canonical (a loaded logit, a bitfield select) costs a quieting
+// v_max_f32 x, x per operand in IEEE mode; logits are never signalling NaNs.
+#ifndef OTH_MS_MAX3
+#define OTH_MS_MAX3 1
+#endif
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+#if OTH_MS_MAX3
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+#else
+    return fmaxf(fmaxf(a, b), c);
+#endif
+}
+__device__ __forceinline__ float vmax2(float a, float b) {
+#if OTH_MS_MAX3
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+#else
+    return fmaxf(a, b);
+#endif
+}
+// max of v[0..K) (exact in any order): a tree of three-input maxima
+template <int K>
+__device__ __forceinline__ float max_reduce(float* v) {
+#pragma unroll
+    for (int w = K; w > 1; w = (w + 2) / 3) {
+#pragma unroll
+        for (int i = 0; 3 * i < w; ++i) {
+            const int k = 3 * i;
+            v[i] = k + 2 < w ? vmax3(v[k], v[k + 1], v[k + 2]) : (k + 1 < w ? vmax2(v[k], v[k + 1]) : v[k]);
+        }
+    }
+    return v[0];
+}
+
 // exp(x - max).  (Folding the shift into fma(x, log2 e, -max log2 e) saves an
 // instruction but leaves exp(0) for the largest logit off 1 by the rounding
 // of max * log2 e, so a lone legal move got a log-prob of +1e-7: not used.)
@@ -206,17 +244,12 @@ __device__ __forceinline__ Pick finish_slot(Slot<CH, G>& b, int l, int NN, const
         full_ent = __logf(fs) - fsx / fs;
     }
     // illegal squares -> -inf: they drop out of the max and get p = exp(-inf) = 0
-    float mb[NB];
+    float mb[NB * 4];
 #pragma unroll
-    for (int bi = 0; bi < NB; ++bi) {
+    for (int bi = 0; bi < NB; ++bi)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) b.x[bi][j] = legal_or_ninf(b.nib[bi], j, b.x[bi][j]);
-        mb[bi] = fmaxf(fmaxf(b.x[bi][0], b.x[bi][1]), fmaxf(b.x[bi][2], b.x[bi][3]));
-    }
-    float m = mb[0];
-#pragma unroll
-    for (int bi = 1; bi < NB; ++bi) m = fmaxf(m, mb[bi]);
-    m = Grp<G>::max(m);
+        for (int j = 0; j < 4; ++j) mb[4 * bi + j] = b.x[bi][j] = legal_or_ninf(b.nib[bi], j, b.x[bi][j]);
+    float m = Grp<G>::max(max_reduce<NB * 4>(mb));
     const bool any = m != -INFINITY;
     const float ms = any ? m : 0.f;
     // p = exp(x - max); tot = sum p; SX = sum p (x - max) (illegal: 0 * -FLT_MAX = 0)
@@ -236,7 +269,7 @@ __device__ __forceinline__ Pick finish_slot(Slot<CH, G>& b, int l, int NN, const
 #pragma unroll
         for (int bi = 0; bi < NB; ++bi)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) sx = fmaf(p[bi][j], fmaxf(b.x[bi][j] - ms, -FLT_MAX), sx);
+            for (int j = 0; j < 4; ++j) sx = fmaf(p[bi][j], vmax2(b.x[bi][j] - ms, -FLT_MAX), sx);
     }
     const float tot = Grp<G>::sum(s);
     const float SX = want_ent ? Grp<G>::sum(sx) : 0.f;
@@ -414,20 +447,15 @@ __device__ __forceinline__ Pick sample_lane(int e, int NN, const float* __restri
         const float FS = tree_sum<G>(fs), FSX = tree_sum<G>(fsx);
         full_ent = __logf(FS) - FSX / FS;
     }
-    float ml[G][NB];  // block maxima: a shallow tree instead of one long fmax chain (the max is exact)
+    float ml[G * NB * 4];  // a shallow tree instead of one long max chain (the max is exact)
 #pragma unroll
     for (int l = 0; l < G; ++l)
 #pragma unroll
-        for (int bi = 0; bi < NB; ++bi) {
+        for (int bi = 0; bi < NB; ++bi)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) x[l][bi][j] = legal_or_ninf(nib[l][bi], j, x[l][bi][j]);
-            ml[l][bi] = fmaxf(fmaxf(x[l][bi][0], x[l][bi][1]), fmaxf(x[l][bi][2], x[l][bi][3]));
-        }
-#pragma unroll
-    for (int w = 1; w < G * NB; w *= 2)
-#pragma unroll
-        for (int i = 0; i + w < G * NB; i += 2 * w) (&ml[0][0])[i] = fmaxf((&ml[0][0])[i], (&ml[0][0])[i + w]);
-    const float m = ml[0][0];
+            for (int j = 0; j < 4; ++j)
+                ml[(l * NB + bi) * 4 + j] = x[l][bi][j] = legal_or_ninf(nib[l][bi], j, x[l][bi][j]);
+    const float m = max_reduce<G * NB * 4>(ml);
     const bool any = m != -INFINITY;
     const float ms = any ? m : 0.f;
     float p[G][NB][4], loc[G][NB], s[G], sx[G];
@@ -452,7 +480,7 @@ __device__ __forceinline__ Pick sample_lane(int e, int NN, const float* __restri
 #pragma unroll
             for (int bi = 0; bi < NB; ++bi)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) sx[l] = fmaf(p[l][bi][j], fmaxf(x[l][bi][j] - ms, -FLT_MAX), sx[l]);
+                for (int j = 0; j < 4; ++j) sx[l] = fmaf(p[l][bi][j], vmax2(x[l][bi][j] - ms, -FLT_MAX), sx[l]);
     }
     const float tot = tree_sum<G>(s);
     const float SX = want_ent ? tree_sum<G>(sx) : 0.f;
@@ -519,6 +547,218 @@ __device__ __forceinline__ Pick sample_lane(int e, int NN, const float* __restri
 #pragma unroll
     for (int c = 0; c < CH; ++c)
         if (a >= 64 * c && a < 64 * c + 64 && a < NN) choice = (words[c] >> (a - 64 * c)) & 1ull;
+    out.lp = (choice && want_lp) ? logits[(size_t)e * (size_t)ld + a] - m - logS : 0.f;
+    out.ent = FULL ? full_ent : ((any && want_ent) ? logS - SX / tot : 0.f);
+    return out;
+}
+
+// The same arithmetic for ONE board computed by a PAIR of lanes (lanes 2k,
+// 2k+1; h = 0, 1): lane h restates the group's lanes 2h and 2h+1 of G = 4
+// (one-word boards) and the pair exchanges partial results through DPP
+// quad_perm [1,0,3,2].  Every combination is the one finish_slot's DPP steps
+// make -- the sum (v0+v1)+(v2+v3) is lane 0's v0+v1 plus lane 1's v2+v3 (an
+// IEEE add is commutative), the exclusive scan of a block is computed whole
+// on both lanes from the four lane values -- so the pick is bit-identical to
+// sample_lane's and k_masked's.  Both lanes return the same Pick.  The caller
+// keeps every branch around the call pair-uniform (DPP reads the partner).
+// The logits rows of a wave's 32 boards (8x8, 16 quads a row) staged through
+// LDS for sample_pair: lane i loads quads i, i+64, ... of the 32 consecutive
+// rows (each load instruction 1 KiB of consecutive rows when ld == 64), all
+// eight loads issued before the first write; quad q = 4bi + 2h + k of row r
+// goes to slot 18r + 9h + 2bi + k, so lane (r, h) reads its eight quads at
+// 18r + 9h + 0..7 and the sixteen lanes of a ds_read_b128 phase hit sixteen
+// distinct bank quads (2r + 9h mod 16).  load_pair_rows issues the loads,
+// store_pair_rows writes them and returns the lane's eight quads.
+constexpr int PAIR_ROW = 18;  // quads per staged row
+__device__ __forceinline__ void load_pair_rows(f32x4 (&v)[8], long long e0, int E, const float* __restrict__ logits,
+                                               long long ld, int lane) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int c = k * 64 + lane, r = c >> 4, q = c & 15;
+        const long long row = e0 + r < E ? e0 + r : E - 1;  // clamped, not branched: the loads stay in flight together
+        v[k] = *reinterpret_cast<const f32x4*>(logits + (size_t)row * (size_t)ld + 4 * q);
+    }
+}
+__device__ __forceinline__ const f32x4* store_pair_rows(f32x4* ws, const f32x4 (&v)[8], int lane) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int c = k * 64 + lane, r = c >> 4, q = c & 15;
+        ws[r * PAIR_ROW + ((q >> 1) & 1) * 9 + ((q >> 2) << 1) + (q & 1)] = v[k];
+    }
+    // a wave reads only what it wrote: LDS operations of one wave complete in order
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return ws + (lane >> 1) * PAIR_ROW + (lane & 1) * 9;
+}
+
+__device__ __forceinline__ float pair_swapf(float x) { return dpp<0xB1>(x); }
+__device__ __forceinline__ int pair_swapi(int x) { return dpp<0xB1>(x); }
+
+template <bool VEC, bool FULL, bool STAGED = false>
+__device__ __forceinline__ Pick sample_pair(int e, int h, int NN, const float* __restrict__ logits, long long ld,
+                                            uint64_t word, const float* __restrict__ uniforms, uint64_t seed,
+                                            uint32_t id_base, uint64_t counter, int mode, bool want_lp,
+                                            bool want_ent, const f32x4* staged = nullptr) {
+    constexpr int G = 4, NB = 4, H = 2;  // the lane's group lanes l = 2h + k, k = 0, 1
+    const float* row = logits + (size_t)e * (size_t)ld;
+    float x[H][NB][4];
+    uint32_t nib[H][NB];
+#pragma unroll
+    for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+        for (int k = 0; k < H; ++k) {
+            const int sq = 4 * G * bi + 4 * (2 * h + k);
+            const int rem = NN - sq;
+            const uint32_t inside = rem >= 4 ? 0xFu : (rem > 0 ? (1u << rem) - 1u : 0u);
+            nib[k][bi] = (uint32_t)(word >> (sq & 63)) & inside;
+            if constexpr (VEC) {
+                f32x4 v = {0.f, 0.f, 0.f, 0.f};
+                if constexpr (STAGED) v = staged[2 * bi + k];  // (8x8: every block inside)
+                else if (sq < NN) v = *reinterpret_cast<const f32x4*>(row + sq);
+                x[k][bi][0] = v.x;
+                x[k][bi][1] = v.y;
+                x[k][bi][2] = v.z;
+                x[k][bi][3] = v.w;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) x[k][bi][j] = sq + j < NN ? row[sq + j] : 0.f;
+            }
+        }
+    float full_ent = 0.f;
+    if constexpr (FULL) {
+        float fm = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < H; ++k)
+#pragma unroll
+            for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (4 * G * bi + 4 * (2 * h + k) + j < NN) fm = fmaxf(fm, x[k][bi][j]);
+        fm = fmaxf(fm, pair_swapf(fm));
+        float fs[H], fsx[H];
+#pragma unroll
+        for (int k = 0; k < H; ++k) {
+            fs[k] = 0.f;
+            fsx[k] = 0.f;
+#pragma unroll
+            for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (4 * G * bi + 4 * (2 * h + k) + j < NN) {
+                        const float d = x[k][bi][j] - fm;
+                        const float q = __expf(d);
+                        fs[k] += q;
+                        fsx[k] = fmaf(q, d, fsx[k]);
+                    }
+        }
+        const float qs = fs[0] + fs[1], qx = fsx[0] + fsx[1];
+        const float FS = qs + pair_swapf(qs), FSX = qx + pair_swapf(qx);
+        full_ent = __logf(FS) - FSX / FS;
+    }
+    float ml[H * NB * 4];
+#pragma unroll
+    for (int k = 0; k < H; ++k)
+#pragma unroll
+        for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) ml[(k * NB + bi) * 4 + j] = x[k][bi][j] = legal_or_ninf(nib[k][bi], j, x[k][bi][j]);
+    float m = max_reduce<H * NB * 4>(ml);
+    m = vmax2(m, pair_swapf(m));
+    const bool any = m != -INFINITY;
+    const float ms = any ? m : 0.f;
+    float p[H][NB][4], loc[H][NB], sl[H], sx[H];
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+        sl[k] = 0.f;
+        sx[k] = 0.f;
+#pragma unroll
+        for (int bi = 0; bi < NB; ++bi) {
+            loc[k][bi] = 0.f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                p[k][bi][j] = exp_shifted(x[k][bi][j], ms);
+                loc[k][bi] += p[k][bi][j];
+            }
+            sl[k] += loc[k][bi];
+        }
+    }
+    if (want_ent) {
+#pragma unroll
+        for (int k = 0; k < H; ++k)
+#pragma unroll
+            for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) sx[k] = fmaf(p[k][bi][j], vmax2(x[k][bi][j] - ms, -FLT_MAX), sx[k]);
+    }
+    const float q = sl[0] + sl[1];
+    const float tot = q + pair_swapf(q);
+    float SX = 0.f;
+    if (want_ent) {
+        const float qx = sx[0] + sx[1];
+        SX = qx + pair_swapf(qx);
+    }
+    const float logS = __logf(tot);
+    int a;
+    if (mode == OTH_MASKED_EVAL) {
+        a = 0;
+    } else {
+        int cand = NONE;
+        if (mode == OTH_MASKED_MODE) {  // the lowest square of the largest legal logit
+#pragma unroll
+            for (int bi = NB - 1; bi >= 0; --bi)
+#pragma unroll
+                for (int k = H - 1; k >= 0; --k)
+#pragma unroll
+                    for (int j = 3; j >= 0; --j)
+                        if (x[k][bi][j] == m) cand = 4 * G * bi + 4 * (2 * h + k) + j;
+        } else {
+            float u;
+            if (uniforms) u = uniforms[e];
+            else u = (float)(oth::philox_x(seed, id_base + (uint32_t)e, counter, RNG_SAMPLE) >> 8) * 0x1p-24f;
+            const float target = u * tot;
+            float carry = 0.f;
+            int cl[H] = {NONE, NONE};
+#pragma unroll
+            for (int bi = 0; bi < NB; ++bi) {
+                const float o0 = pair_swapf(loc[0][bi]), o1 = pair_swapf(loc[1][bi]);
+                float v[G], scan[G];
+                v[0] = h ? o0 : loc[0][bi];
+                v[1] = h ? o1 : loc[1][bi];
+                v[2] = h ? loc[0][bi] : o0;
+                v[3] = h ? loc[1][bi] : o1;
+                excl_scan_lanes<G>(v, scan);
+#pragma unroll
+                for (int k = 0; k < H; ++k) {
+                    float cdf = carry + (h ? scan[2 + k] : scan[k]);
+                    uint32_t below = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        cdf += p[k][bi][j];
+                        below += cdf <= target ? 1u : 0u;
+                    }
+                    const uint32_t hit = nib[k][bi] & (0xFu << below);
+                    if (cl[k] == NONE && hit) cl[k] = 4 * G * bi + 4 * (2 * h + k) + __builtin_ctz(hit);
+                }
+                if (bi + 1 < NB) carry += tree_sum<G>(v);
+            }
+            cand = ::min(cl[0], cl[1]);
+        }
+        cand = ::min(cand, pair_swapi(cand));
+        if (cand == NONE && any) {  // u * total rounded up to the total: the last legal square
+            int last = -1;
+#pragma unroll
+            for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+                for (int k = 0; k < H; ++k)
+                    if (nib[k][bi]) last = ::max(last, 4 * G * bi + 4 * (2 * h + k) + 31 - __builtin_clz(nib[k][bi]));
+            cand = ::max(last, pair_swapi(last));
+        }
+        a = any ? cand : 0;
+    }
+    Pick out;
+    out.a = a;
+    const bool choice = a >= 0 && a < NN && ((word >> (a & 63)) & 1ull);
     out.lp = (choice && want_lp) ? logits[(size_t)e * (size_t)ld + a] - m - logS : 0.f;
     out.ent = FULL ? full_ent : ((any && want_ent) ? logS - SX / tot : 0.f);
     return out;

@@ -13,6 +13,7 @@ import ctypes
 import torch
 
 from . import _lib as L
+from .masked import _rows
 
 _OBS_LAYOUTS = {"board": L.OTH_OBS_BOARD, "board_legal": L.OTH_OBS_BOARD_LEGAL,
                 "make_state": L.OTH_OBS_MAKE_STATE, "absolute": L.OTH_OBS_ABSOLUTE}
@@ -24,6 +25,9 @@ _POLICIES = {"random": L.OTH_POLICY_RANDOM, "greedy": L.OTH_POLICY_GREEDY,
              "maximin3": L.OTH_POLICY_MAXIMIN3}
 
 BLACK_DISK, NO_DISK, WHITE_DISK = -1, 0, 1  # othello.py:10-12
+
+
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 
 
 def nwords(n):
@@ -75,6 +79,8 @@ class VecOthelloEnv(object):
 
     # ------------------------------------------------------------------ utils
     def _stream(self):
+        if _RAW_STREAM is not None:  # the current stream's handle without building a Stream object
+            return ctypes.c_void_p(_RAW_STREAM(self.device.index))
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
     def close(self):
@@ -93,6 +99,19 @@ class VecOthelloEnv(object):
 
     def _u8(self, *shape):
         return torch.empty(*shape, dtype=torch.uint8, device=self.device)
+
+    def _out(self, given, dtype, name):
+        """An (E,) output: a new tensor for None / True, nothing for False, or the
+        caller's tensor (checked) to be written in place."""
+        if given is None or given is True:
+            return torch.empty(self.num_envs, dtype=dtype, device=self.device)
+        if given is False:
+            return None
+        if given.dtype != dtype or given.numel() != self.num_envs or not given.is_contiguous() or \
+                given.device != self.device:
+            raise ValueError("%s must be a contiguous %s tensor of %d elements on %s" %
+                             (name, dtype, self.num_envs, self.device))
+        return given
 
     @property
     def ply_counter(self):
@@ -292,22 +311,25 @@ class VecOthelloEnv(object):
         return acts, lp, ent
 
     def sample_step(self, logits, deterministic=False, uniforms=None, log_probs=True, entropy=True,
-                    full_entropy=False, rewards=None, dones=None):
+                    full_entropy=False, rewards=None, dones=None, actions=None):
         """sample_actions(logits) then step(actions) in ONE launch (oth_sample_step):
         Policy.act (model.py:60-99) over every board's possible_moves followed by
         OthelloBaseEnv.step (othello.py:412-462), bit-identical to the two calls.
-        Returns (actions int32, log_probs, entropy, rewards int32, dones bool)."""
-        from .masked import _rows
+        Returns (actions int32, log_probs, entropy, rewards int32, dones bool).
+        Outputs may be given to be written in place: `actions` / `rewards` int32 (E,),
+        `dones` uint8 (E,), and `log_probs` / `entropy` as float32 (E,) tensors
+        instead of True."""
         x = _rows(logits, self.board_size)
         if x.shape[0] != self.num_envs:
             raise ValueError("logits must have one row per board")
-        if uniforms is not None:
+        if uniforms is not None and (uniforms.dtype != torch.float32 or not uniforms.is_contiguous() or
+                                     uniforms.device != x.device):
             uniforms = uniforms.to(device=x.device, dtype=torch.float32).contiguous()
-        acts = self._i32(self.num_envs)
-        lp = torch.empty(self.num_envs, dtype=torch.float32, device=self.device) if log_probs else None
-        ent = torch.empty(self.num_envs, dtype=torch.float32, device=self.device) if entropy else None
-        r = rewards if rewards is not None else self._i32(self.num_envs)
-        d = dones if dones is not None else self._u8(self.num_envs)
+        acts = self._out(actions, torch.int32, "actions")
+        lp = self._out(log_probs, torch.float32, "log_probs")
+        ent = self._out(entropy, torch.float32, "entropy")
+        r = self._out(rewards, torch.int32, "rewards")
+        d = self._out(dones, torch.uint8, "dones")
         mode = (L.OTH_MASKED_MODE if deterministic else L.OTH_MASKED_SAMPLE) | \
             (L.OTH_MASKED_FULL_ENTROPY if full_entropy else 0)
         L.check(self._lib.oth_sample_step(self._h, _ptr(x), x.stride(0), _ptr(uniforms), self._sample_calls, mode,

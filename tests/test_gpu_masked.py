@@ -266,7 +266,8 @@ def test_masked_matches_reference_policy_heads(torch_gpu, golden_dir, n_board):
         assert np.min(np.abs(cdf - u[i])) < CDF_TOL, (i, a[i], ref[i])
 
 
-@pytest.mark.parametrize("n_board,E", [(8, 65536), (6, 3001), (10, 4096), (16, 1000)])
+@pytest.mark.parametrize("n_board,E", [(8, 65536), (6, 3001), (7, 2049), (5, 1500), (4, 999), (10, 4096),
+                                       (16, 1000)])
 def test_sample_step_equals_sample_then_step(torch_gpu, n_board, E):
     """oth_sample_step (one launch: k_masked's sampler + OthelloBaseEnv.step)
     is bit-identical to sample_actions followed by step: actions, log-probs,
@@ -330,3 +331,32 @@ def test_sample_step_graph_region_replays(torch_gpu):
         assert torch.equal(out_g, out_e)
         for x, y in zip(graphed.get_state(), eager.get_state()):
             assert torch.equal(x, y)
+
+
+def test_sample_step_writes_given_outputs(torch_gpu):
+    """Outputs handed to sample_step are written in place and equal fresh ones;
+    a wrong dtype / size is refused before any launch."""
+    torch = torch_gpu
+    from gymothelloenv_amd import VecOthelloEnv
+    E, n = 1000, 8
+    dev = torch.device("cuda", 0)
+    logits = torch.randn(E, n * n, device=dev, generator=torch.Generator(device=dev).manual_seed(2))
+    kw = dict(board_size=n, auto_reset=True, seed=4, device=dev)
+    a, b = VecOthelloEnv(E, **kw), VecOthelloEnv(E, **kw)
+    a.reset()
+    b.reset()
+    acts = torch.full((E,), -7, dtype=torch.int32, device=dev)
+    lp = torch.empty(E, device=dev)
+    ent = torch.empty(E, device=dev)
+    rew = torch.empty(E, dtype=torch.int32, device=dev)
+    don = torch.empty(E, dtype=torch.uint8, device=dev)
+    for _ in range(5):
+        out = a.sample_step(logits, actions=acts, log_probs=lp, entropy=ent, rewards=rew, dones=don)
+        ref = b.sample_step(logits)
+        assert out[0] is acts and out[1] is lp and out[2] is ent and out[3] is rew
+        for x, y in zip(out, ref):
+            assert torch.equal(x, y)
+    with pytest.raises(ValueError):
+        a.sample_step(logits, actions=torch.empty(E, dtype=torch.int64, device=dev))
+    with pytest.raises(ValueError):
+        a.sample_step(logits, log_probs=torch.empty(E - 1, device=dev))

@@ -38,12 +38,14 @@ def main():
     u = torch.rand(K, E, device=dev, generator=g)
     rew = torch.empty(E, dtype=torch.int32, device=dev)
     don = torch.empty(E, dtype=torch.uint8, device=dev)
+    acts = torch.empty(E, dtype=torch.int32, device=dev)
 
     def plies(env):
         for k in range(K):
             uk = None if a.device_draws else u[k]
             if a.fused:
-                env.sample_step(logits, uniforms=uk, log_probs=False, entropy=False, rewards=rew, dones=don)
+                env.sample_step(logits, uniforms=uk, log_probs=False, entropy=False, rewards=rew, dones=don,
+                                actions=acts)
             else:
                 act, _, _ = env.sample_actions(logits, uniforms=uk, log_probs=False, entropy=False)
                 env.step(act, rewards=rew, dones=don, observe=False)
