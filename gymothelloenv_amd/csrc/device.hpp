@@ -105,6 +105,9 @@ using namespace oth;
 #ifndef OTH_SS2_STAGE
 #define OTH_SS2_STAGE 1  // k_sample_step2 (8x8): the wave's logits rows through LDS, coalesced loads
 #endif
+#ifndef OTH_PLAY_PAIR
+#define OTH_PLAY_PAIR 0  // 1: k_play_rand on lane pairs (k_play_rand2, PairFills): bit-identical but 8x8 0.78 -> 0.98 us per ply (233 VALU per lane-ply vs 308 per board-ply; two waves reach 3.7 cycles per VALU per SIMD, one wave 5.5)
+#endif
 #ifndef OTH_SS_ABL
 #define OTH_SS_ABL 0
 #endif
@@ -1200,6 +1203,256 @@ __device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_
             rl = (uint32_t)scale_index(philox_x(rng.seed, id, g, RNG_OPENING_AUTO), rng.init_rand / 2 + 1) * 2u;
         meta = (rl & 0xffu) << M_RAND_SHIFT;
     }
+}
+
+// PairFills<N>: the Fills engine on a lane pair (lanes 2k, 2k+1; h = 0, 1),
+// one-word boards.  Lane h scans two of the four axes -- h = 0 the E/W and
+// S/N axes, h = 1 the two diagonals -- on dword pairs with per-lane shift
+// amounts (v_lshlrev_b32 / v_alignbit_b32 take the amount from a register, so
+// both lanes run one instruction stream), keeps the fills of its four ray
+// directions and computes their flips from the ray tables (the directions
+// toward lower squares on the turned board, as Fills with OTH_FLIP_TURN 2);
+// moves and flips are or-ed through the pair's DPP swap.  Twice the lanes per
+// board: two waves share each SIMD at 65,536 boards, where one wave alone
+// issues at half the SIMD's rate.
+template <int N>
+struct PairFills {
+    static_assert(Geo<N>::W == 1, "pair fills are for one-word boards (N <= 8)");
+    static constexpr int STEPS = Pro<N, 0, 1>::STEPS;
+    static_assert(STEPS <= 3, "1 + 1 + 2 + 2 doubling");
+    static constexpr uint64_t BD = Geo<N>::BOARD.w[0], IN = Geo<N>::INNER.w[0];
+    const uint64_t* rays;  // lds + 128 h: ray tables of directions 2h, 2h + 1 (+256: the turned 4 + 2h, 5 + 2h)
+    uint32_t sA, rA, sA2, rA2, sB, rB, sB2, rB2;  // axis shifts s, 32 - s, 2s, 32 - 2s
+    U2 mB;                                        // axis B's propagator mask (the vertical axis: whole board)
+    mutable U2 tu[2], td[2];                      // fills of up directions 2h + j and down directions 4 + 2h + j
+    __device__ __forceinline__ PairFills(int h, const uint64_t* lds) {
+        rays = lds + 128 * h;
+        sA = h ? N + 1 : 1;
+        sB = h ? N - 1 : N;
+        rA = 32 - sA;
+        rB = 32 - sB;
+        sA2 = 2 * sA;
+        rA2 = 32 - sA2;
+        sB2 = 2 * sB;
+        rB2 = 32 - sB2;
+        mB = u2(h ? IN : BD);
+    }
+    __device__ __forceinline__ static U2 shl(U2 x, uint32_t s, uint32_t r) {
+        return U2{x.lo << s, __builtin_amdgcn_alignbit(x.hi, x.lo, r)};
+    }
+    __device__ __forceinline__ static U2 shr(U2 x, uint32_t s) {
+        return U2{__builtin_amdgcn_alignbit(x.hi, x.lo, s), x.hi >> s};
+    }
+    // OneWord::axis with the shift in registers
+    __device__ __forceinline__ static void axis(U2 P, U2 p1, uint32_t s, uint32_t r, uint32_t s2, uint32_t r2,
+                                                U2& L, U2& tplus, U2& tminus) {
+        U2 p2{0u, 0u};
+        if constexpr (STEPS > 1) p2 = p1 & shl(p1, s, r);
+        U2 x = shl(P, s, r) & p1;
+        x = (p1 & shl(x, s, r)) | x;
+        if constexpr (STEPS > 1) x = (p2 & shl(x, s2, r2)) | x;
+        if constexpr (STEPS > 2) x = (p2 & shl(x, s2, r2)) | x;
+        tplus = x;
+        L = L | shl(x, s, r);
+        const U2 p2m = shr(p2, s);
+        x = shr(P, s) & p1;
+        x = (p1 & shr(x, s)) | x;
+        if constexpr (STEPS > 1) x = (p2m & shr(x, s2)) | x;
+        if constexpr (STEPS > 2) x = (p2m & shr(x, s2)) | x;
+        tminus = x;
+        L = L | shr(x, s);
+    }
+    // get_possible_actions (othello.py:313-343) for mover Pw; the lane's fills kept
+    __device__ __forceinline__ uint64_t legal(uint64_t Pw, uint64_t Ow) const {
+        const U2 P = u2(Pw), O = u2(Ow);
+        U2 L{0u, 0u};
+        axis(P, O & u2(IN), sA, rA, sA2, rA2, L, td[0], tu[0]);
+        axis(P, O & mB, sB, rB, sB2, rB2, L, td[1], tu[1]);
+        const uint64_t l = u64(L);
+        return (l | pair_swap(l)) & ~(Pw | Ow) & BD;
+    }
+    // update_board's flips (othello.py:391-410) from square a (Fills::flip's form)
+    __device__ __forceinline__ uint64_t flip(int a) const {
+        const uint64_t* r = rays + a;
+        uint64_t f = 0, g = 0;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint64_t ray = r[64 * j], t = u64(tu[j]);
+            f |= and3_64(ray, t, (ray & ~t) - 1ull);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint64_t ray = r[256 + 64 * j], tt = OneWord<N>::turn180(u64(td[j]));
+            g |= and3_64(ray, tt, (ray & ~tt) - 1ull);
+        }
+        f |= OneWord<N>::turn180(g);
+        return f | pair_swap(f);
+    }
+};
+
+// The reset position's moves and the lane's fills, computed once per launch.
+template <int N>
+struct PairStart {
+    uint64_t L;
+    U2 tu[2], td[2];
+};
+
+// play_rand_fast on a lane pair (random policy): both lanes hold the board and
+// take the same pick; the scan and the flips are split (PairFills).
+template <int N, bool OPEN>
+__device__ __forceinline__ void play_rand_pair(uint64_t& M, uint64_t& O, uint64_t& L, uint32_t& meta,
+                                               const PairFills<N>& eng, const PairStart<N>& st, uint32_t u,
+                                               uint32_t flags, const Rng& rng, uint32_t id, uint64_t g, int& a,
+                                               int& r, int& d, uint32_t& cb, uint32_t& cd, uint32_t& cw) {
+    constexpr uint64_t BD = Geo<N>::BOARD.w[0];
+    constexpr int NN = N * N;
+    a = select64(L, scale_index(u, popc64(L)));  // RandomPolicy (simple_policies.py:37-41); L != 0
+    if constexpr (OPEN) meta -= (meta & 0xff00u) ? (1u << M_RAND_SHIFT) : 0u;
+    const uint64_t m = 1ull << a;
+    const uint64_t f = eng.flip(a);  // update_board (othello.py:391-410)
+    const uint64_t Mn = M | f | m, On = O & ~f;
+    const bool full = (Mn | On) == BD;  // :425-426
+    uint64_t Ln = eng.legal(On, Mn);    // the opponent's possible_moves (:436)
+    const bool pass = Ln == 0 && !full;
+    if (pass) Ln = eng.legal(Mn, On);  // :437-440 (pair-uniform: Ln is the pair's or)
+    const bool term = full || Ln == 0;
+    const bool swap = !pass && !full;
+    M = swap ? On : Mn;
+    O = swap ? Mn : On;
+    L = Ln;
+    meta ^= swap ? M_TURN_WHITE : 0u;
+    r = 0;
+    d = term ? 1 : 0;
+    if (term) {
+        const bool tw = (meta & M_TURN_WHITE) != 0;
+        const int pc = popc64(Mn), oc = popc64(On);
+        if (flags & OTH_DISK_REWARD) r = oc == 0 ? NN : pc - oc;
+        else r = pc > oc ? 1 : (pc < oc ? -1 : 0);
+        const bool mover_wins = pc > oc, opp_wins = pc < oc;
+        cb += tw ? opp_wins : mover_wins;
+        cd += !mover_wins && !opp_wins;
+        cw += tw ? mover_wins : opp_wins;
+        M = Start<N>::BLACK.w[0];
+        O = Start<N>::WHITE.w[0];
+        L = st.L;
+        eng.tu[0] = st.tu[0];
+        eng.tu[1] = st.tu[1];
+        eng.td[0] = st.td[0];
+        eng.td[1] = st.td[1];
+        uint32_t rl = 0;
+        if (rng.init_rand > 0)
+            rl = (uint32_t)scale_index(philox_x(rng.seed, id, g, RNG_OPENING_AUTO), rng.init_rand / 2 + 1) * 2u;
+        meta = (rl & 0xffu) << M_RAND_SHIFT;
+    }
+}
+
+// k_play_rand<N> on lane pairs (random policy, auto-reset, every output): the
+// same plies, draws and outputs; both lanes of a pair store the same values.
+template <int N>
+__global__ __launch_bounds__(BLOCK) void k_play_rand2(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
+                                                      uint64_t* __restrict__ legal, int E, uint32_t flags, int plies,
+                                                      int32_t* __restrict__ actions, int32_t* __restrict__ rewards,
+                                                      uint8_t* __restrict__ dones,
+                                                      unsigned long long* __restrict__ wdl, Rng rng, uint64_t ply0) {
+    static_assert(Geo<N>::W == 1, "one-word boards");
+    ply0 += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
+    __shared__ __attribute__((aligned(16))) uint64_t lds_rays[8 * 64];
+    const int gt = blockIdx.x * BLOCK + threadIdx.x;
+    const int e = gt >> 1, h = gt & 1;
+    Lane<N> s;
+    if (e < E) load_lane<N>(s, boards, meta, legal, e);
+    fill_rays<N, true>(lds_rays);
+    uint32_t cb = 0, cd = 0, cw = 0;
+    if (e < E) {  // pair-uniform
+        const uint32_t id = rng.id_base + (uint32_t)e;
+        const PairFills<N> eng(h, lds_rays);
+        PairStart<N> st;
+        st.L = eng.legal(Start<N>::BLACK.w[0], Start<N>::WHITE.w[0]);
+        st.tu[0] = eng.tu[0];
+        st.tu[1] = eng.tu[1];
+        st.td[0] = eng.td[0];
+        st.td[1] = eng.td[1];
+        const bool tw0 = (s.meta & M_TURN_WHITE) != 0;
+        uint64_t M = tw0 ? s.white.w[0] : s.black.w[0];
+        uint64_t O = tw0 ? s.black.w[0] : s.white.w[0];
+        uint64_t L = s.legal.w[0];
+        uint32_t mt = s.meta & (0xff00u | M_TURN_WHITE);
+        (void)eng.legal(M, O);  // the mover's fills
+        const bool slow = __any((s.meta & M_TERMINATED) != 0);
+        int32_t* act_p = actions + e;
+        int32_t* rew_p = rewards + e;
+        uint8_t* done_p = dones + e;
+        auto fast = [&](auto OPENC) __attribute__((always_inline)) {
+            constexpr bool OPEN = decltype(OPENC)::value;
+            auto ply = [&](int p, uint32_t u) __attribute__((always_inline)) {
+                int a, r, d;
+                play_rand_pair<N, OPEN>(M, O, L, mt, eng, st, u, flags, rng, id, ply0 + (uint64_t)p, a, r, d, cb, cd,
+                                        cw);
+                *act_p = a;  // both lanes of the pair: the same value to the same address
+                *rew_p = r;
+                *done_p = (uint8_t)d;
+                act_p += E;
+                rew_p += E;
+                done_p += E;
+            };
+            int p = 0;
+            while (p < plies && ((ply0 + (uint64_t)p) & 3) != 0) {
+                const uint64_t g = ply0 + (uint64_t)p;
+                ply(p, pick4(philox4(rng.seed, id, g >> 2, RNG_ACTION), (uint32_t)(g & 3)));
+                ++p;
+            }
+            if (p + 4 <= plies) {
+                U4 cur = philox4(rng.seed, id, (ply0 + (uint64_t)p) >> 2, RNG_ACTION);
+                while (p + 4 <= plies) {
+                    const U4 nxt = p + 8 <= plies ? philox4(rng.seed, id, ((ply0 + (uint64_t)p) >> 2) + 1, RNG_ACTION)
+                                                  : cur;
+                    ply(p, cur.x);
+                    ply(p + 1, cur.y);
+                    ply(p + 2, cur.z);
+                    ply(p + 3, cur.w);
+                    cur = nxt;
+                    p += 4;
+                }
+            }
+            while (p < plies) {
+                const uint64_t g = ply0 + (uint64_t)p;
+                ply(p, pick4(philox4(rng.seed, id, g >> 2, RNG_ACTION), (uint32_t)(g & 3)));
+                ++p;
+            }
+        };
+        if (!slow) {
+            if (OTH_OPEN_SPLIT && rng.init_rand == 0 && !__any((mt & 0xff00u) != 0)) fast(std::false_type{});
+            else fast(std::true_type{});
+            const bool tw = (mt & M_TURN_WHITE) != 0;
+            s.white.w[0] = tw ? M : O;
+            s.black.w[0] = tw ? O : M;
+            s.legal.w[0] = L;
+            s.meta = mt;
+        } else {  // a board loaded terminated in the wave (k_play's semantics): both lanes step alone
+            const Solo<N> solo(0, nullptr);
+            for (int p = 0; p < plies; ++p) {
+                const uint64_t g = ply0 + (uint64_t)p;
+                int a = -1, r = 0, d = 1, win = NO_DISK;
+                if (!(s.meta & M_TERMINATED)) {
+                    a = random_action<N>(s, action_draw(rng.seed, id, g));
+                    if ((s.meta >> M_RAND_SHIFT) > 0) s.meta -= 1u << M_RAND_SHIFT;
+                    step_lane<N>(s, a, flags, r, d, win, solo);
+                    if (d) {
+                        cb += win == BLACK_DISK;
+                        cd += win == NO_DISK;
+                        cw += win == WHITE_DISK;
+                        reset_lane<N>(s, rng.seed, id, g, RNG_OPENING_AUTO, rng.init_rand);
+                    }
+                }
+                act_p[(size_t)p * E] = a;
+                rew_p[(size_t)p * E] = r;
+                done_p[(size_t)p * E] = (uint8_t)d;
+            }
+        }
+        if (h == 0) store_lane<N>(s, boards, meta, legal, e);
+    }
+    if (h) cb = cd = cw = 0;  // one count per board
+    tally(wdl, cb, cd, cw);
 }
 
 template <int N, int POLICY = OTH_POLICY_RANDOM>

@@ -58,6 +58,12 @@ void launch_k_play(int lanes_per_board, oth_env* env, int n_plies, int32_t* acti
     const dim3 grid(grid_for((long long)lanes_per_board * env->E)), block(BLOCK);
     if constexpr (OTH_FAST_RANDOM && POL == OTH_POLICY_RANDOM && std::is_same<Eng, Fills<N>>::value) {
         if (actions && rewards && dones && (env->flags & OTH_AUTO_RESET)) {
+            if (OTH_PLAY_PAIR && grid_for(2LL * env->E) <= env->nslots) {  // lane pairs (k_play_rand2)
+                hipLaunchKernelGGL((k_play_rand2<N>), dim3(grid_for(2LL * env->E)), block, 0, st, env->boards,
+                                   env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards, dones,
+                                   env->wdl, rng_of(env), ply0);
+                return;
+            }
             hipLaunchKernelGGL((k_play_rand<N>), grid, block, 0, st, env->boards, env->meta, env->legal, env->E,
                                env->flags, n_plies, actions, rewards, dones, env->wdl, rng_of(env), ply0);
             return;
