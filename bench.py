@@ -155,6 +155,17 @@ def load_pmc(workload):
         return None
 
 
+def play_kernel_name(n, policy, record):
+    """The kernel oth_step_policy launches for this configuration (kernels_n.hip
+    launch_k_play): the restructured auto-reset kernels when every per-ply
+    output is stored, else the generic k_play."""
+    if record and policy in ("random", "greedy") and n <= 8:
+        return "k_play_rand<%d,%s>" % (n, policy)
+    if record and policy == "random":
+        return "k_play_rand_w<%d>" % n
+    return "k_play<%d,%s>" % (n, policy)
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -346,7 +357,7 @@ def main(argv=None):
             "roofline": {"bound": "valu-issue", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS,
                          "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
-                         "kernel": "k_play<%d,%s>" % (n, args.policy), "avg_launch_us": avg_launch_s * 1e6,
+                         "kernel": play_kernel_name(n, args.policy, record), "avg_launch_us": avg_launch_s * 1e6,
                          "launches_timed": args.steps,
                          "algorithmic_bytes_per_env_step": bps,
                          "algorithmic_bytes_per_launch": alg_launch,
