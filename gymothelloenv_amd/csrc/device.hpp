@@ -108,6 +108,9 @@ using namespace oth;
 #ifndef OTH_PLAY_PAIR
 #define OTH_PLAY_PAIR 0  // 1: k_play_rand on lane pairs (k_play_rand2, PairFills): bit-identical but 8x8 0.78 -> 0.98 us per ply (233 VALU per lane-ply vs 308 per board-ply; two waves reach 3.7 cycles per VALU per SIMD, one wave 5.5)
 #endif
+#ifndef OTH_SS2_SOLO
+#define OTH_SS2_SOLO 0  // k_sample_step2: step with Solo on each lane instead of Duo
+#endif
 #ifndef OTH_SS_ABL
 #define OTH_SS_ABL 0
 #endif
@@ -1858,18 +1861,39 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step2(uint64_t* __restrict__ b
     __shared__ __attribute__((aligned(16))) uint64_t lds_rays[Duo<N>::RAY_WORDS];
     const long long gt = (long long)blockIdx.x * BLOCK + threadIdx.x;
     const int e = (int)(gt >> 1), h = (int)(gt & 1);
-    const Duo<N> eng(h, lds_rays);
+    // the step's engine: Duo (half the axes and rays per lane) or, OTH_SS2_SOLO, each lane the whole
+    // step (the pair's lanes agree: same inputs) without ray tables, LDS or a barrier
+    using Eng = typename std::conditional<OTH_SS2_SOLO != 0, Solo<N>, Duo<N>>::type;
+    const Eng eng(h, lds_rays);
     uint32_t cb = 0, cd = 0, cw = 0;
     Lane<N> s;  // the board's loads are issued first, in flight with the logits loads
     if (e < E) load_lane<N>(s, boards, meta, legal, e);
     auto board = [&](auto STAGEDC, const oth_ms::f32x4* staged) __attribute__((always_inline)) {
         if (e >= E) return;  // pair-uniform: both lanes of a pair share e
+#if OTH_SS_ABL  // timing ablations (tools/ab_sample_step.py --no-check): 1 no sampling, 2 loads only, 3 no step
+        oth_ms::Pick pk{s.legal.w[0] ? (int)__builtin_ctzll(s.legal.w[0]) : 0, 0.f, 0.f};
+        if (OTH_SS_ABL == 2) {
+            const float* rw = logits + (size_t)e * (size_t)ld + 32 * h;
+            float acc = 0.f;
+#pragma unroll
+            for (int q = 0; q < 32; q += 4) {
+                const oth_ms::f32x4 v = *reinterpret_cast<const oth_ms::f32x4*>(rw + q);
+                acc += (v.x + v.y) + (v.z + v.w);
+            }
+            if (acc == 12345.f) pk.a = 1;
+        }
+        if (OTH_SS_ABL == 3)
+            pk = oth_ms::sample_pair<VEC, FULL, decltype(STAGEDC)::value>(
+                e, h, NN, logits, ld, s.legal.w[0], uniforms, rng.seed, rng.id_base, counter, mode,
+                log_probs != nullptr, entropy != nullptr, staged);
+#else
         const oth_ms::Pick pk = oth_ms::sample_pair<VEC, FULL, decltype(STAGEDC)::value>(
             e, h, NN, logits, ld, s.legal.w[0], uniforms, rng.seed, rng.id_base, counter, mode, log_probs != nullptr,
             entropy != nullptr, staged);
+#endif
         const bool was_term = (s.meta & M_TERMINATED) != 0;
-        int r, d, win;
-        step_lane<N>(s, pk.a, flags, r, d, win, eng);
+        int r = 0, d = 0, win = NO_DISK;
+        if (OTH_SS_ABL != 3) step_lane<N>(s, pk.a, flags, r, d, win, eng);
         if (d && !was_term) {
             if (h == 0) {
                 cb = win == BLACK_DISK;
@@ -1894,12 +1918,12 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step2(uint64_t* __restrict__ b
         const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
         oth_ms::f32x4 v[8];
         oth_ms::load_pair_rows(v, (gt - lane) >> 1, E, logits, ld, lane);
-        fill_rays<N, false, false>(lds_rays);  // while the rows are in flight
+        if constexpr (!OTH_SS2_SOLO) fill_rays<N, false, false>(lds_rays);  // while the rows are in flight
         const oth_ms::f32x4* rows = oth_ms::store_pair_rows(stage + wv * 32 * oth_ms::PAIR_ROW, v, lane);
         __syncthreads();  // the ray tables (the rows need only the wave's own order)
         board(std::true_type{}, rows);
     } else {
-        fill_rays<N, false>(lds_rays);
+        if constexpr (!OTH_SS2_SOLO) fill_rays<N, false>(lds_rays);
         board(std::false_type{}, nullptr);
     }
     tally(wdl, cb, cd, cw);

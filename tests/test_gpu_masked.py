@@ -360,3 +360,33 @@ def test_sample_step_writes_given_outputs(torch_gpu):
         a.sample_step(logits, actions=torch.empty(E, dtype=torch.int64, device=dev))
     with pytest.raises(ValueError):
         a.sample_step(logits, log_probs=torch.empty(E - 1, device=dev))
+
+
+@pytest.mark.parametrize("n_board,E", [(8, 2049), (8, 40000), (7, 40000), (6, 20000)])
+def test_sample_step_without_auto_reset(torch_gpu, n_board, E):
+    """Every lane layout of oth_sample_step (quads up to 16,384 boards, pairs for
+    7x7 / 8x8 beyond, one lane otherwise) against sample_actions + step without
+    auto-reset: games end and stay terminated with stale possible_moves, the
+    sampler still draws on them, step answers done with reward 0
+    (othello.py:415-416), both flag settings of the rewards."""
+    torch = torch_gpu
+    from gymothelloenv_amd import VecOthelloEnv
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(E + n_board)
+    for disk in (False, True):
+        kw = dict(board_size=n_board, auto_reset=False, num_disk_as_reward=disk, seed=5, device=dev)
+        fused, split = VecOthelloEnv(E, **kw), VecOthelloEnv(E, **kw)
+        fused.reset()
+        split.reset()
+        for k in range(n_board * n_board + 4):
+            logits = torch.randn(E, n_board * n_board, device=dev, generator=g)
+            uni = torch.rand(E, device=dev, generator=g)
+            a1, lp1, en1, r1, d1 = fused.sample_step(logits, uniforms=uni)
+            a2, lp2, en2 = split.sample_actions(logits, uniforms=uni)
+            _, r2, d2, _ = split.step(a2, observe=False)
+            assert torch.equal(a1, a2) and torch.equal(lp1, lp2) and torch.equal(en1, en2), k
+            assert torch.equal(r1, r2) and torch.equal(d1, d2), k
+        for x, y in zip(fused.get_state(), split.get_state()):
+            assert torch.equal(x, y)
+        assert bool(d1.all())  # every game over after N*N plies
+        assert torch.equal(fused.counts(), split.counts())
