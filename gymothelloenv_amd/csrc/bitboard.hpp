@@ -538,8 +538,15 @@ OTH_HD BB<Geo<N>::W> legal_moves(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O)
 // opponent discs only (d = 0..3: E, S, SE, SW toward higher squares; 4..7: W,
 // N, NW, NE).  The scan stepping +S from the own discs yields the fill of
 // direction -S and vice versa.
+#ifndef OTH_DW_SCAN
+#define OTH_DW_SCAN 4  // multi-word boards of up to this many words: legal_moves_fills on dwords (legal_moves_fills_dw)
+#endif
+template <int N>
+OTH_HD BB<Geo<N>::W> legal_moves_fills_dw(const BB<Geo<N>::W>& Pb, const BB<Geo<N>::W>& Ob, BB<Geo<N>::W> t[8]);
+
 template <int N>
 OTH_HD BB<Geo<N>::W> legal_moves_fills(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O, BB<Geo<N>::W> t[8]) {
+    if constexpr (Geo<N>::W >= 2 && Geo<N>::W <= OTH_DW_SCAN) return legal_moves_fills_dw<N>(P, O, t);
     auto L = zero<Geo<N>::W>();
     const auto pin = O & Geo<N>::INNER;
     legal_axis<N, 1>(P, pin, L, t[4], t[0]);      // W / E
@@ -547,6 +554,153 @@ OTH_HD BB<Geo<N>::W> legal_moves_fills(const BB<Geo<N>::W>& P, const BB<Geo<N>::
     legal_axis<N, N + 1>(P, pin, L, t[6], t[2]);  // NW / SE
     legal_axis<N, N - 1>(P, pin, L, t[7], t[3]);  // NE / SW
     return L & ~(P | O) & Geo<N>::BOARD;
+}
+
+// Multi-word boards (N = 9..16) on dwords (DW<2W>): legal_axis's arithmetic
+// with every multi-word shift as one v_lshlrev / v_alignbit per dword (a
+// funnel shift across the dword boundary) instead of 64-bit shifts plus the
+// cross-word carries, and and-or pairs as v_and_or_b32 / v_bitop3_b32.
+template <int K>
+struct DW {
+    uint32_t d[K];
+};
+template <int W>
+OTH_HD DW<2 * W> to_dw(const BB<W>& b) {
+    DW<2 * W> q;
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+        q.d[2 * i] = (uint32_t)b.w[i];
+        q.d[2 * i + 1] = (uint32_t)(b.w[i] >> 32);
+    }
+    return q;
+}
+template <int K>
+OTH_HD BB<K / 2> to_bb(const DW<K>& q) {
+    BB<K / 2> b;
+#pragma unroll
+    for (int i = 0; i < K / 2; ++i) b.w[i] = ((uint64_t)q.d[2 * i + 1] << 32) | q.d[2 * i];
+    return b;
+}
+template <int K>
+OTH_HD DW<K> operator&(const DW<K>& a, const DW<K>& b) {
+    DW<K> r;
+#pragma unroll
+    for (int i = 0; i < K; ++i) r.d[i] = a.d[i] & b.d[i];
+    return r;
+}
+template <int K>
+OTH_HD DW<K> operator|(const DW<K>& a, const DW<K>& b) {
+    DW<K> r;
+#pragma unroll
+    for (int i = 0; i < K; ++i) r.d[i] = a.d[i] | b.d[i];
+    return r;
+}
+template <int K>
+OTH_HD DW<K> operator~(const DW<K>& a) {
+    DW<K> r;
+#pragma unroll
+    for (int i = 0; i < K; ++i) r.d[i] = ~a.d[i];
+    return r;
+}
+// (hi:lo) >> c, low dword (c in 1..31)
+OTH_HD uint32_t funnel_hd(uint32_t hi, uint32_t lo, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_alignbit(hi, lo, c);
+#else
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> c);
+#endif
+}
+template <int S, int K>  // S > 0: toward higher squares
+OTH_HD DW<K> sh(const DW<K>& x) {
+    DW<K> y;
+    if constexpr (S >= 0) {
+        constexpr int q = S / 32, r = S % 32;
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            const int src = i - q;
+            if (src < 0) y.d[i] = 0u;
+            else if (r == 0) y.d[i] = x.d[src];
+            else if (src == 0) y.d[i] = x.d[0] << r;
+            else y.d[i] = funnel_hd(x.d[src], x.d[src - 1], 32 - r);
+        }
+    } else {
+        constexpr int q = (-S) / 32, r = (-S) % 32;
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            const int src = i + q;
+            if (src > K - 1) y.d[i] = 0u;
+            else if (r == 0) y.d[i] = x.d[src];
+            else if (src == K - 1) y.d[i] = x.d[K - 1] >> r;
+            else y.d[i] = funnel_hd(x.d[src + 1], x.d[src], r);
+        }
+    }
+    return y;
+}
+
+// legal_axis on dwords (the same steps, propagators and reuse)
+template <int N, int S, int K = 2 * Geo<N>::W>
+OTH_HD void legal_axis_dw(const DW<K>& P, const DW<K>& p1, DW<K>& L, DW<K>& tplus, DW<K>& tminus) {
+    constexpr int STEPS = Pro<N, 0, 1>::STEPS;
+    constexpr bool R3 = OTH_PROP_REUSE && STEPS == 3 && Geo<N>::MAXRUN <= 6;
+    constexpr bool R4 = OTH_PROP_REUSE && STEPS == 4 && Geo<N>::MAXRUN <= 12;
+    DW<K> p2{}, p4{}, p8{};
+    if constexpr (STEPS > 1) p2 = p1 & sh<S>(p1);
+    if constexpr (STEPS > 2 && !R3) p4 = p2 & sh<2 * S>(p2);
+    if constexpr (STEPS > 3 && !R4) p8 = p4 & sh<4 * S>(p4);
+    {
+        DW<K> t = sh<S>(P) & p1;
+        t = (p1 & sh<S>(t)) | t;
+        if constexpr (STEPS > 1) t = (p2 & sh<2 * S>(t)) | t;
+        if constexpr (STEPS > 2) {
+            if constexpr (R3) t = (p2 & sh<2 * S>(t)) | t;
+            else t = (p4 & sh<4 * S>(t)) | t;
+        }
+        if constexpr (STEPS > 3) {
+            if constexpr (R4) t = (p4 & sh<4 * S>(t)) | t;
+            else t = (p8 & sh<8 * S>(t)) | t;
+        }
+        tplus = t;
+        L = L | sh<S>(t);
+    }
+    {
+        DW<K> t = sh<-S>(P) & p1;
+        t = (p1 & sh<-S>(t)) | t;
+        DW<K> p2m{}, p4m{};
+        if constexpr (STEPS > 1) {
+            p2m = sh<-S>(p2);
+            t = (p2m & sh<-2 * S>(t)) | t;
+        }
+        if constexpr (STEPS > 2) {
+            if constexpr (R3) {
+                t = (p2m & sh<-2 * S>(t)) | t;
+            } else {
+                p4m = sh<-3 * S>(p4);
+                t = (p4m & sh<-4 * S>(t)) | t;
+            }
+        }
+        if constexpr (STEPS > 3) {
+            if constexpr (R4) t = (p4m & sh<-4 * S>(t)) | t;
+            else t = (sh<-7 * S>(p8) & sh<-8 * S>(t)) | t;
+        }
+        tminus = t;
+        L = L | sh<-S>(t);
+    }
+}
+
+// legal_moves_fills for multi-word boards on dwords (fills returned as words)
+template <int N>
+OTH_HD BB<Geo<N>::W> legal_moves_fills_dw(const BB<Geo<N>::W>& Pb, const BB<Geo<N>::W>& Ob, BB<Geo<N>::W> t[8]) {
+    constexpr int W = Geo<N>::W, K = 2 * W;
+    static_assert(W >= 2, "multi-word boards");
+    const DW<K> P = to_dw<W>(Pb), O = to_dw<W>(Ob), pin = O & to_dw<W>(Geo<N>::INNER);
+    DW<K> L{}, f[8];
+    legal_axis_dw<N, 1>(P, pin, L, f[4], f[0]);
+    legal_axis_dw<N, N>(P, O, L, f[5], f[1]);
+    legal_axis_dw<N, N + 1>(P, pin, L, f[6], f[2]);
+    legal_axis_dw<N, N - 1>(P, pin, L, f[7], f[3]);
+#pragma unroll
+    for (int d = 0; d < 8; ++d) t[d] = to_bb<K>(f[d]);
+    return to_bb<K>(L & ~(P | O) & to_dw<W>(Geo<N>::BOARD));
 }
 
 // update_board's flips (othello.py:391-410) from the fills of the side to
