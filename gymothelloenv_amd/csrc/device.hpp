@@ -114,6 +114,9 @@ using namespace oth;
 #ifndef OTH_SS_ABL
 #define OTH_SS_ABL 0
 #endif
+#ifndef OTH_RAYS_REP
+#define OTH_RAYS_REP 0  // k_play_rand (N <= 8): flips from the lane-replicated ray table (FillsRep, conflict-free ds_read_b128)
+#endif
 #ifndef OTH_FLIP_TURN
 #define OTH_FLIP_TURN 2  // Fills::flip toward lower squares on the board turned by 180 degrees, no 64-bit clz (2: turned rays tabled under the unturned square, +3 % at 8x8; 1: addressed at NN-1-a, -1.5 %)
 #endif
@@ -431,6 +434,71 @@ struct Fills {
         (void)legal(pick(tw, s.white, s.black), pick(tw, s.black, s.white));
     }
     __device__ __forceinline__ bool leader() const { return true; }
+};
+
+// FillsRep<N> (k_play_rand, OTH_RAYS_REP): Fills whose flips read the ray
+// tables from 16 copies laid out so that every lane of a wave reads a 16-byte
+// slot of the LDS bank row of its own.  Entry (sq, k) holds the rays of
+// directions 2k, 2k+1 (k = 2, 3: the turned rays of 4..7, as OTH_FLIP_TURN 2)
+// at byte sq*1024 + k*256 + 16*(lane & 15): a flip is four ds_read_b128 with
+// immediate offsets, and the 16 lanes of each of ds_read_b128's lane groups
+// ({0-3,12-15,20-27}, ...) hit 16 distinct slots whatever squares they play:
+// conflict-free, 4 LDS cycles a read, against 8 plus the random squares' bank
+// conflicts for each ds_read2st64_b64 pair from the 4-KiB table.  64 KiB of
+// LDS per block (two 256-lane blocks per CU).
+constexpr int REP_ENTRIES = 64 * 4 * 16;
+template <int N>
+__device__ __forceinline__ void fill_rays_rep(ulonglong2* rep) {
+    static_assert(OTH_FLIP_TURN == 2, "the replicated table holds the turned rays");
+    for (int i = threadIdx.x; i < 64 * 4; i += BLOCK) {
+        const int sq = i >> 2, k = i & 3;
+        uint64_t r2[2] = {0, 0};
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int d = 2 * k + j;
+            if (sq < N * N) {
+                const int dr = __builtin_amdgcn_sbfe((int)0xFFF01110u, 4 * d, 4);
+                const int dc = __builtin_amdgcn_sbfe((int)0x1F0FF101u, 4 * d, 4);
+                int row = sq / N + dr, col = sq % N + dc;
+                while (row >= 0 && row < N && col >= 0 && col < N) {
+                    const int s2 = row * N + col;
+                    r2[j] |= 1ull << (d >= 4 ? N * N - 1 - s2 : s2);
+                    row += dr;
+                    col += dc;
+                }
+            }
+        }
+        ulonglong2 v;
+        v.x = r2[0];
+        v.y = r2[1];
+        // slot (s + i) & 15: eight consecutive threads write eight distinct slots
+#pragma unroll
+        for (int s = 0; s < 16; ++s) rep[i * 16 + ((s + i) & 15)] = v;
+    }
+    __syncthreads();
+}
+template <int N>
+struct FillsRep : Fills<N> {
+    const ulonglong2* rep;  // + (lane & 15)
+    __device__ __forceinline__ FillsRep(const uint64_t* lds, const ulonglong2* rp)
+        : Fills<N>(0, lds), rep(rp + (threadIdx.x & 15)) {}
+    __device__ __forceinline__ BB<1> flip(const BB<1>&, const BB<1>&, int a) const {
+        const ulonglong2* r = rep + a * 64;
+        const ulonglong2 v0 = r[0], v1 = r[16], v2 = r[32], v3 = r[48];
+        const uint64_t* t = this->t;
+        const uint64_t up[4] = {v0.x, v0.y, v1.x, v1.y}, dn[4] = {v2.x, v2.y, v3.x, v3.y};
+        uint64_t f = 0, g = 0;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) f |= and3_64(up[d], t[d], (up[d] & ~t[d]) - 1ull);  // as Fills::flip
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const uint64_t tt = OneWord<N>::turn180(t[4 + d]);
+            g |= and3_64(dn[d], tt, (dn[d] & ~tt) - 1ull);
+        }
+        BB<1> out;
+        out.w[0] = f | OneWord<N>::turn180(g);
+        return out;
+    }
 };
 
 // FillsW<N>: the Fills engine for multi-word boards (N >= 9): the legal scan
@@ -1145,9 +1213,9 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
 // OPEN: some board of the wave may have random-opening plies left (the
 // handle's initial_rand_steps > 0, or a board loaded with some); without, the
 // opening bookkeeping is compiled out.
-template <int N, int POLICY = OTH_POLICY_RANDOM, bool OPEN = true>
+template <int N, int POLICY = OTH_POLICY_RANDOM, bool OPEN = true, typename Eng = Fills<N>>
 __device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_t& L, uint32_t& meta,
-                                               const Fills<N>& eng, uint32_t u, uint32_t flags, const Rng& rng,
+                                               const Eng& eng, uint32_t u, uint32_t flags, const Rng& rng,
                                                uint32_t id, uint64_t g, int& a, int& r, int& d, uint32_t& cb,
                                                uint32_t& cd, uint32_t& cw) {
     constexpr uint64_t BD = Geo<N>::BOARD.w[0];
@@ -1467,12 +1535,22 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
     static_assert(Geo<N>::W == 1, "one-word boards");
     ply0 += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
     __shared__ __attribute__((aligned(16))) uint64_t lds_rays[Fills<N>::RAY_WORDS];
+#if OTH_RAYS_REP
+    __shared__ __attribute__((aligned(16))) ulonglong2 lds_rep[REP_ENTRIES];
+    fill_rays<N, turned_rays<Fills<N>>::value, false>(lds_rays);  // the generic loop's table (boards loaded terminated)
+    fill_rays_rep<N>(lds_rep);
+#else
     fill_rays<N, turned_rays<Fills<N>>::value>(lds_rays);
+#endif
     const int e = blockIdx.x * BLOCK + threadIdx.x;
     uint32_t cb = 0, cd = 0, cw = 0;
     if (e < E) {
         const uint32_t id = rng.id_base + (uint32_t)e;
+#if OTH_RAYS_REP
+        const FillsRep<N> eng(lds_rays, lds_rep);
+#else
         const Fills<N> eng(0, lds_rays);
+#endif
         Lane<N> s;
         load_lane<N>(s, boards, meta, legal, e);
         const bool tw0 = (s.meta & M_TURN_WHITE) != 0;
@@ -1492,7 +1570,7 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
         auto ply = [&](int p, uint32_t u) __attribute__((always_inline)) {
             int a, r, d;
             play_rand_fast<N, POLICY, OPEN>(M, O, L, mt, eng, u, flags, rng, id, ply0 + (uint64_t)p, a, r, d, cb, cd,
-                                            cw);
+                                            cw);  // (Eng deduced: FillsRep with OTH_RAYS_REP)
             *act_p = a;
             *rew_p = r;
             *done_p = (uint8_t)d;
