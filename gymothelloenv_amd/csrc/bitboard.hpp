@@ -511,8 +511,21 @@ OTH_HD void legal_axis(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& p1, BB<Geo<N
 // which some direction holds >= 1 opponent disc followed by an own disc.
 // Written as rays cast FROM the mover's discs; the set of (square, direction)
 // pairs it accepts is the same as the reference's per-cell scan.
+#ifndef OTH_DW_SCAN
+#define OTH_DW_SCAN 4  // multi-word boards of up to this many words: legal_moves_fills on dwords (legal_moves_fills_dw)
+#endif
+#ifndef OTH_DW_LEGAL
+#define OTH_DW_LEGAL 1  // legal_moves (Solo: k_step, k_sample_step, k_step_vs, ...) on dwords too for multi-word boards
+#endif
+template <int N>
+OTH_HD BB<Geo<N>::W> legal_moves_fills_dw(const BB<Geo<N>::W>& Pb, const BB<Geo<N>::W>& Ob, BB<Geo<N>::W> t[8]);
+
 template <int N>
 OTH_HD BB<Geo<N>::W> legal_moves(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O) {
+    if constexpr (Geo<N>::W >= 2 && Geo<N>::W <= OTH_DW_SCAN && OTH_DW_LEGAL) {
+        BB<Geo<N>::W> t[8];  // the fills are dead here
+        return legal_moves_fills_dw<N>(P, O, t);
+    }
     auto L = zero<Geo<N>::W>();
 #if OTH_AXIS_LEGAL
     const auto pin = O & Geo<N>::INNER;
@@ -538,12 +551,6 @@ OTH_HD BB<Geo<N>::W> legal_moves(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O)
 // opponent discs only (d = 0..3: E, S, SE, SW toward higher squares; 4..7: W,
 // N, NW, NE).  The scan stepping +S from the own discs yields the fill of
 // direction -S and vice versa.
-#ifndef OTH_DW_SCAN
-#define OTH_DW_SCAN 4  // multi-word boards of up to this many words: legal_moves_fills on dwords (legal_moves_fills_dw)
-#endif
-template <int N>
-OTH_HD BB<Geo<N>::W> legal_moves_fills_dw(const BB<Geo<N>::W>& Pb, const BB<Geo<N>::W>& Ob, BB<Geo<N>::W> t[8]);
-
 template <int N>
 OTH_HD BB<Geo<N>::W> legal_moves_fills(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O, BB<Geo<N>::W> t[8]) {
     if constexpr (Geo<N>::W >= 2 && Geo<N>::W <= OTH_DW_SCAN) return legal_moves_fills_dw<N>(P, O, t);
