@@ -108,6 +108,12 @@ using namespace oth;
 #ifndef OTH_PLAY_PAIR
 #define OTH_PLAY_PAIR 0  // 1: k_play_rand on lane pairs (k_play_rand2, PairFills): bit-identical but 8x8 0.78 -> 0.98 us per ply (233 VALU per lane-ply vs 308 per board-ply; two waves reach 3.7 cycles per VALU per SIMD, one wave 5.5)
 #endif
+#ifndef OTH_SS_PAIR_W
+#define OTH_SS_PAIR_W 1  // oth_sample_step on lane pairs for two-word boards too (N = 9..11; Solo step on both lanes)
+#endif
+#ifndef OTH_SS_PAIR_W_MAX_E
+#define OTH_SS_PAIR_W_MAX_E 32768  // two-word boards whose rows are not float4-aligned: pairs up to this many boards
+#endif
 #ifndef OTH_SS2_SOLO
 #define OTH_SS2_SOLO 0  // k_sample_step2: step with Solo on each lane instead of Duo
 #endif
@@ -1932,16 +1938,19 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step2(uint64_t* __restrict__ b
                                                         float* __restrict__ log_probs, float* __restrict__ entropy,
                                                         int32_t* __restrict__ rewards, uint8_t* __restrict__ dones,
                                                         unsigned long long* __restrict__ wdl, Rng rng, uint64_t ply) {
-    static_assert(Geo<N>::W == 1 && OTH_MS_G == 4, "lane pairs restate k_masked's four lanes of one-word boards");
+    constexpr int W = Geo<N>::W;
+    static_assert(W <= 2 && OTH_MS_G == 4, "lane pairs restate k_masked's four lanes of boards of <= 2 words");
     constexpr int NN = N * N;
     ply += rng.ply_off[0];      // graph-region offsets (oth_graph_end); 0 eagerly
     counter += rng.ply_off[1];  // the sample counter's, as k_masked
-    __shared__ __attribute__((aligned(16))) uint64_t lds_rays[Duo<N>::RAY_WORDS];
+    // the step's engine: Duo (one-word boards: half the axes and rays per lane) or, OTH_SS2_SOLO and
+    // on two-word boards, each lane the whole step (the pair's lanes agree: same inputs) without ray
+    // tables, LDS or a barrier
+    constexpr bool SOLO = OTH_SS2_SOLO != 0 || W == 2;
+    using Eng = typename std::conditional<SOLO, Solo<N>, Duo<N>>::type;
+    __shared__ __attribute__((aligned(16))) uint64_t lds_rays[SOLO ? 1 : 8 * 64];
     const long long gt = (long long)blockIdx.x * BLOCK + threadIdx.x;
     const int e = (int)(gt >> 1), h = (int)(gt & 1);
-    // the step's engine: Duo (half the axes and rays per lane) or, OTH_SS2_SOLO, each lane the whole
-    // step (the pair's lanes agree: same inputs) without ray tables, LDS or a barrier
-    using Eng = typename std::conditional<OTH_SS2_SOLO != 0, Solo<N>, Duo<N>>::type;
     const Eng eng(h, lds_rays);
     uint32_t cb = 0, cd = 0, cw = 0;
     Lane<N> s;  // the board's loads are issued first, in flight with the logits loads
@@ -1961,12 +1970,12 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step2(uint64_t* __restrict__ b
             if (acc == 12345.f) pk.a = 1;
         }
         if (OTH_SS_ABL == 3)
-            pk = oth_ms::sample_pair<VEC, FULL, decltype(STAGEDC)::value>(
-                e, h, NN, logits, ld, s.legal.w[0], uniforms, rng.seed, rng.id_base, counter, mode,
+            pk = oth_ms::sample_pair<W, VEC, FULL, decltype(STAGEDC)::value>(
+                e, h, NN, logits, ld, s.legal.w, uniforms, rng.seed, rng.id_base, counter, mode,
                 log_probs != nullptr, entropy != nullptr, staged);
 #else
-        const oth_ms::Pick pk = oth_ms::sample_pair<VEC, FULL, decltype(STAGEDC)::value>(
-            e, h, NN, logits, ld, s.legal.w[0], uniforms, rng.seed, rng.id_base, counter, mode, log_probs != nullptr,
+        const oth_ms::Pick pk = oth_ms::sample_pair<W, VEC, FULL, decltype(STAGEDC)::value>(
+            e, h, NN, logits, ld, s.legal.w, uniforms, rng.seed, rng.id_base, counter, mode, log_probs != nullptr,
             entropy != nullptr, staged);
 #endif
         const bool was_term = (s.meta & M_TERMINATED) != 0;
@@ -1996,12 +2005,12 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step2(uint64_t* __restrict__ b
         const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
         oth_ms::f32x4 v[8];
         oth_ms::load_pair_rows(v, (gt - lane) >> 1, E, logits, ld, lane);
-        if constexpr (!OTH_SS2_SOLO) fill_rays<N, false, false>(lds_rays);  // while the rows are in flight
+        if constexpr (!SOLO) fill_rays<N, false, false>(lds_rays);  // while the rows are in flight
         const oth_ms::f32x4* rows = oth_ms::store_pair_rows(stage + wv * 32 * oth_ms::PAIR_ROW, v, lane);
         __syncthreads();  // the ray tables (the rows need only the wave's own order)
         board(std::true_type{}, rows);
     } else {
-        if constexpr (!OTH_SS2_SOLO) fill_rays<N, false>(lds_rays);
+        if constexpr (!SOLO) fill_rays<N, false>(lds_rays);
         board(std::false_type{}, nullptr);
     }
     tally(wdl, cb, cd, cw);

@@ -142,11 +142,18 @@ void launch_ss(oth_env* env, const float* logits, long long ld, const float* uni
     }
     // lane pairs (k_sample_step2) for 7x7 and 8x8: 8x8 7.77 -> 7.22 us per ply graphed (-8.5 % with
     // log-probs); 6x6 loses (5.1 -> 6.0: the one-lane form folds the squares past N*N away)
-    if constexpr (Geo<N>::W == 1 && N >= 7 && OTH_SS_PAIR) {
-        hipLaunchKernelGGL((k_sample_step2<N, VEC, FULL>), dim3(grid_for(2LL * env->E)), dim3(BLOCK), 0, st,
-                           env->boards, env->meta, env->legal, env->E, env->flags, logits, ld, uniforms, counter, mode,
-                           actions, log_probs, entropy, rewards, dones, env->wdl, rng_of(env), ply);
-        return;
+    // two-word boards (9x9 .. 11x11): pairs for float4-aligned rows (10x10: 11.62 -> 11.42 us at 65,536
+    // boards) and up to OTH_SS_PAIR_W_MAX_E boards otherwise (9x9 / 11x11 at 16,384: -14 / -20 %; at
+    // 65,536 the pairs' scalar loads lose 9 %); 10x10 at 777 .. 32,768 boards: -20 .. -25 %
+    constexpr bool PAIR1 = Geo<N>::W == 1 && N >= 7 && OTH_SS_PAIR;
+    constexpr bool PAIR2 = Geo<N>::W == 2 && OTH_SS_PAIR_W;
+    if constexpr (PAIR1 || PAIR2) {
+        if (PAIR1 || VEC || env->E <= OTH_SS_PAIR_W_MAX_E) {
+            hipLaunchKernelGGL((k_sample_step2<N, VEC, FULL>), dim3(grid_for(2LL * env->E)), dim3(BLOCK), 0, st,
+                               env->boards, env->meta, env->legal, env->E, env->flags, logits, ld, uniforms, counter,
+                               mode, actions, log_probs, entropy, rewards, dones, env->wdl, rng_of(env), ply);
+            return;
+        }
     }
     constexpr bool ONE = OTH_SS_ONE && Geo<N>::W <= 2;
     const long long lanes = ONE ? (long long)env->E : ((long long)env->E + G - 1) / G * G;

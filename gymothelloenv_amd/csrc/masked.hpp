@@ -595,12 +595,13 @@ __device__ __forceinline__ const f32x4* store_pair_rows(f32x4* ws, const f32x4 (
 __device__ __forceinline__ float pair_swapf(float x) { return dpp<0xB1>(x); }
 __device__ __forceinline__ int pair_swapi(int x) { return dpp<0xB1>(x); }
 
-template <bool VEC, bool FULL, bool STAGED = false>
+template <int CH, bool VEC, bool FULL, bool STAGED = false>
 __device__ __forceinline__ Pick sample_pair(int e, int h, int NN, const float* __restrict__ logits, long long ld,
-                                            uint64_t word, const float* __restrict__ uniforms, uint64_t seed,
-                                            uint32_t id_base, uint64_t counter, int mode, bool want_lp,
-                                            bool want_ent, const f32x4* staged = nullptr) {
-    constexpr int G = 4, NB = 4, H = 2;  // the lane's group lanes l = 2h + k, k = 0, 1
+                                            const uint64_t (&words)[CH], const float* __restrict__ uniforms,
+                                            uint64_t seed, uint32_t id_base, uint64_t counter, int mode,
+                                            bool want_lp, bool want_ent, const f32x4* staged = nullptr) {
+    static_assert(CH <= 2, "k_masked's four lanes per board cover up to 128 squares");
+    constexpr int G = 4, NB = 4 * CH, H = 2;  // the lane's group lanes l = 2h + k, k = 0, 1
     const float* row = logits + (size_t)e * (size_t)ld;
     float x[H][NB][4];
     uint32_t nib[H][NB];
@@ -611,7 +612,7 @@ __device__ __forceinline__ Pick sample_pair(int e, int h, int NN, const float* _
             const int sq = 4 * G * bi + 4 * (2 * h + k);
             const int rem = NN - sq;
             const uint32_t inside = rem >= 4 ? 0xFu : (rem > 0 ? (1u << rem) - 1u : 0u);
-            nib[k][bi] = (uint32_t)(word >> (sq & 63)) & inside;
+            nib[k][bi] = (uint32_t)(words[sq >> 6] >> (sq & 63)) & inside;
             if constexpr (VEC) {
                 f32x4 v = {0.f, 0.f, 0.f, 0.f};
                 if constexpr (STAGED) v = staged[2 * bi + k];  // (8x8: every block inside)
@@ -758,7 +759,10 @@ __device__ __forceinline__ Pick sample_pair(int e, int h, int NN, const float* _
     }
     Pick out;
     out.a = a;
-    const bool choice = a >= 0 && a < NN && ((word >> (a & 63)) & 1ull);
+    bool choice = false;
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+        if (a >= 64 * c && a < 64 * c + 64 && a < NN) choice = (words[c] >> (a - 64 * c)) & 1ull;
     out.lp = (choice && want_lp) ? logits[(size_t)e * (size_t)ld + a] - m - logS : 0.f;
     out.ent = FULL ? full_ent : ((any && want_ent) ? logS - SX / tot : 0.f);
     return out;

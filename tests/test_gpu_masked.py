@@ -267,7 +267,7 @@ def test_masked_matches_reference_policy_heads(torch_gpu, golden_dir, n_board):
 
 
 @pytest.mark.parametrize("n_board,E", [(8, 65536), (6, 3001), (7, 2049), (5, 1500), (4, 999), (10, 4096),
-                                       (16, 1000)])
+                                       (9, 777), (11, 3001), (9, 40000), (16, 1000)])
 def test_sample_step_equals_sample_then_step(torch_gpu, n_board, E):
     """oth_sample_step (one launch: k_masked's sampler + OthelloBaseEnv.step)
     is bit-identical to sample_actions followed by step: actions, log-probs,
@@ -362,10 +362,10 @@ def test_sample_step_writes_given_outputs(torch_gpu):
         a.sample_step(logits, log_probs=torch.empty(E - 1, device=dev))
 
 
-@pytest.mark.parametrize("n_board,E", [(8, 2049), (8, 40000), (7, 40000), (6, 20000)])
+@pytest.mark.parametrize("n_board,E", [(8, 2049), (8, 40000), (7, 40000), (6, 20000), (10, 5001)])
 def test_sample_step_without_auto_reset(torch_gpu, n_board, E):
     """Every lane layout of oth_sample_step (quads up to 16,384 boards, pairs for
-    7x7 / 8x8 beyond, one lane otherwise) against sample_actions + step without
+    7x7 / 8x8 beyond and for two-word boards, one lane otherwise) against sample_actions + step without
     auto-reset: games end and stay terminated with stale possible_moves, the
     sampler still draws on them, step answers done with reward 0
     (othello.py:415-416), both flag settings of the rewards."""
