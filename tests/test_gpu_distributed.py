@@ -52,3 +52,62 @@ def test_rccl_wdl_all_gather_single_rank():
     assert d["backend"] == "nccl"
     assert d["gathered"] == [d["local"]] and d["total"] == d["local"]
     assert sum(d["local"]) >= 65536 and d["max"] == 1.5
+
+
+CHILD2 = r"""
+import hashlib, json, os, sys
+sys.path.insert(0, %(root)r)
+import torch, torch.distributed as dist
+dist.init_process_group("gloo")
+from gymothelloenv_amd.distributed import ShardedVecOthelloEnv
+env = ShardedVecOthelloEnv(%(G)d, board_size=8, auto_reset=True, seed=11, initial_rand_steps=4, device="cuda:0")
+env.reset()
+acts, _, _ = env.step_policy("random", n_plies=%(P)d)
+b, m, lg = env.get_state()
+torch.cuda.synchronize()
+print(json.dumps({"rank": env.rank, "base": env.env_id_base, "n": env.num_envs,
+                  "acts": hashlib.sha256(acts.cpu().numpy().tobytes()).hexdigest(),
+                  "boards": hashlib.sha256(b.cpu().numpy().tobytes()).hexdigest(),
+                  "local": env.counts().cpu().tolist(), "total": env.global_counts().cpu().tolist()}), flush=True)
+dist.destroy_process_group()
+"""
+
+
+def test_two_ranks_on_one_gpu_equal_one_process():
+    """The product's multi-rank path with two ranks (gloo: RCCL takes one rank
+    per device) sharing cuda:0: each rank's ShardedVecOthelloEnv shard plays
+    exactly the boards [base, base + n) of a one-process run at the same
+    global E (actions, final boards), and the all-gathered W/D/L equals the
+    one-process tally (ppo_run_self_play.py:432-441)."""
+    import hashlib
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from gymothelloenv_amd import VecOthelloEnv
+    G, P = 9001, 90  # ragged: the first rank takes one board more
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-c", CHILD2 % {"root": ROOT, "G": G, "P": P}], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        so, se = p.communicate(timeout=100)
+        assert p.returncode == 0, se[-3000:]
+        outs.append(json.loads(so.strip().splitlines()[-1]))
+    ref = VecOthelloEnv(G, board_size=8, auto_reset=True, seed=11, initial_rand_steps=4, device="cuda:0")
+    ref.reset()
+    acts, _, _ = ref.step_policy("random", n_plies=P)
+    b, _, _ = ref.get_state()
+    acts, b = acts.cpu().numpy(), b.cpu().numpy()
+    for d in sorted(outs, key=lambda d: d["rank"]):
+        lo, hi = d["base"], d["base"] + d["n"]
+        assert hashlib.sha256(acts[:, lo:hi].copy().tobytes()).hexdigest() == d["acts"], d["rank"]
+        assert hashlib.sha256(b[lo:hi].copy().tobytes()).hexdigest() == d["boards"], d["rank"]
+        assert d["total"] == ref.counts().cpu().tolist()
+    assert [o["n"] for o in sorted(outs, key=lambda d: d["rank"])] == [4501, 4500]
+    assert [sum(x) for x in zip(*(o["local"] for o in outs))] == ref.counts().cpu().tolist()
