@@ -2,8 +2,9 @@
 travels with the repo snapshot to the GPU box).
 
 The kernels are templates over the board size N; csrc/kernels_n.hip is
-compiled once per N (-DOTH_N=4..16) in parallel, csrc/capi.hip holds the C
-ABI, and the objects are linked into one shared library.
+compiled once per N (-DOTH_N=4..16) in parallel, csrc/play_rand_n.hip (the
+bench kernel, its own scheduler flags) once per N = 4..8, csrc/capi.hip holds
+the C ABI, and the objects are linked into one shared library.
 
 Reproducibility: objects go to a fixed directory (`_objs/`, git-ignored) so the
 compiler's per-TU ids (derived from the input path and options) are the same on
@@ -23,7 +24,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 SIZES = list(range(4, 17))
-SOURCES = ("capi.hip", "kernels_n.hip", "masked.hip", "device.hpp", "launch.hpp", "bitboard.hpp", "masked.hpp")
+SOURCES = ("capi.hip", "kernels_n.hip", "play_rand_n.hip", "masked.hip", "device.hpp", "launch.hpp", "bitboard.hpp",
+           "masked.hpp")
+PLAY_SIZES = list(range(4, 9))  # k_play_rand: one-word boards
+# play_rand_n.hip: the max-ILP machine scheduler (one wave per SIMD: latency hidden by the schedule
+# counts, occupancy does not); the rest of the library keeps the default scheduler
+PLAY_FLAGS = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
 DEPS = [os.path.join(CSRC, f) for f in SOURCES] + [os.path.join(ROOT, "include", "othello_mi355x.h")]
 OUT = os.path.join(HERE, "liboth_mi355x.so")
 OBJDIR = os.path.join(HERE, "_objs")
@@ -41,7 +47,7 @@ def source_hash(extra_flags=()):
         with open(p, "rb") as f:
             h.update(f.read())
         h.update(b"\0")
-    h.update(" ".join([ARCH] + BASE_FLAGS + list(extra_flags)).encode())
+    h.update(" ".join([ARCH] + BASE_FLAGS + PLAY_FLAGS + list(extra_flags)).encode())
     return h.hexdigest()
 
 
@@ -77,6 +83,8 @@ def build(force=False, verbose=True, extra_flags=(), out=OUT, jobs=None):
              (os.path.join(CSRC, "masked.hip"), os.path.join(objdir, "masked.o"), [])]
     units += [(os.path.join(CSRC, "kernels_n.hip"), os.path.join(objdir, "kernels_n%d.o" % n), ["-DOTH_N=%d" % n])
               for n in SIZES]
+    units += [(os.path.join(CSRC, "play_rand_n.hip"), os.path.join(objdir, "play_rand_n%d.o" % n),
+               ["-DOTH_N=%d" % n] + PLAY_FLAGS) for n in PLAY_SIZES]
 
     def compile_one(u):
         src, obj, defs = u

@@ -87,6 +87,9 @@ using namespace oth;
 #ifndef OTH_FAST_RANDOM_W
 #define OTH_FAST_RANDOM_W 1  // k_play_rand_w: the same restructured random play for multi-word boards (N >= 9)
 #endif
+#ifndef OTH_RAND_FILL
+#define OTH_RAND_FILL 1  // k_play_rand: the next Philox block computed after the first ply's scan (its region)
+#endif
 #ifndef OTH_RAND_PIPE
 #define OTH_RAND_PIPE 1  // k_play_rand: the next Philox block computed inside the current 4-ply group
 #endif
@@ -1219,11 +1222,17 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
 // OPEN: some board of the wave may have random-opening plies left (the
 // handle's initial_rand_steps > 0, or a board loaded with some); without, the
 // opening bookkeeping is compiled out.
-template <int N, int POLICY = OTH_POLICY_RANDOM, bool OPEN = true, typename Eng = Fills<N>>
+struct NoFill {
+    __device__ __forceinline__ void operator()() const {}
+};
+// FILL: independent work (the next Philox block) run after the opponent's scan
+// and pinned there, so that it shares the ply's first scheduling region with the
+// pick, the ray-table loads, the flips and the scan (OTH_RAND_FILL)
+template <int N, int POLICY = OTH_POLICY_RANDOM, bool OPEN = true, typename Eng = Fills<N>, typename FILL = NoFill>
 __device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_t& L, uint32_t& meta,
                                                const Eng& eng, uint32_t u, uint32_t flags, const Rng& rng,
                                                uint32_t id, uint64_t g, int& a, int& r, int& d, uint32_t& cb,
-                                               uint32_t& cd, uint32_t& cw) {
+                                               uint32_t& cd, uint32_t& cw, const FILL& fill = FILL{}) {
     constexpr uint64_t BD = Geo<N>::BOARD.w[0];
     constexpr int NN = N * N;
     if constexpr (POLICY == OTH_POLICY_RANDOM) {
@@ -1245,6 +1254,7 @@ __device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_
     pb.w[0] = On;
     ob.w[0] = Mn;
     uint64_t Ln = eng.legal(pb, ob).w[0];  // the opponent's possible_moves (:436), fills kept in eng.t
+    fill();
     const bool pass = Ln == 0 && !full;
     if (pass) {  // :437-440: the mover moves again (fills recomputed for the mover)
         pb.w[0] = Mn;
@@ -1573,10 +1583,10 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
         uint8_t* done_p = dones + e;
         auto fast = [&](auto OPENC) __attribute__((always_inline)) {
         constexpr bool OPEN = decltype(OPENC)::value;
-        auto ply = [&](int p, uint32_t u) __attribute__((always_inline)) {
+        auto ply = [&](int p, uint32_t u, const auto& fill) __attribute__((always_inline)) {
             int a, r, d;
             play_rand_fast<N, POLICY, OPEN>(M, O, L, mt, eng, u, flags, rng, id, ply0 + (uint64_t)p, a, r, d, cb, cd,
-                                            cw);  // (Eng deduced: FillsRep with OTH_RAYS_REP)
+                                            cw, fill);  // (Eng deduced: FillsRep with OTH_RAYS_REP)
             *act_p = a;
             *rew_p = r;
             *done_p = (uint8_t)d;
@@ -1584,8 +1594,9 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
             rew_p += E;
             done_p += E;
         };
+        const NoFill nofill;
         if (POLICY != OTH_POLICY_RANDOM) {  // scripted policy: draws only on opening plies
-            for (int p = 0; p < plies; ++p) ply(p, 0u);
+            for (int p = 0; p < plies; ++p) ply(p, 0u, nofill);
             return;
         }
         int p = 0;
@@ -1595,25 +1606,36 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
             // its independent VALU work fills the wait for the ray-table loads.
             while (p < plies && ((ply0 + (uint64_t)p) & 3) != 0) {
                 const uint64_t g = ply0 + (uint64_t)p;
-                ply(p, pick4(philox4(rng.seed, id, g >> 2, RNG_ACTION), (uint32_t)(g & 3)));
+                ply(p, pick4(philox4(rng.seed, id, g >> 2, RNG_ACTION), (uint32_t)(g & 3)), nofill);
                 ++p;
             }
             if (p + 4 <= plies) {
                 U4 cur = philox4(rng.seed, id, (ply0 + (uint64_t)p) >> 2, RNG_ACTION);
                 while (p + 4 <= plies) {
+#if OTH_RAND_FILL
+                    // the next block (one unused after the last group) computed in the first
+                    // ply's region, pinned before its pass test
+                    U4 nxt;
+                    const uint64_t nb = ((ply0 + (uint64_t)p) >> 2) + 1;
+                    ply(p, cur.x, [&]() __attribute__((always_inline)) {
+                        nxt = philox4(rng.seed, id, nb, RNG_ACTION);
+                        asm volatile("" : "+v"(nxt.x), "+v"(nxt.y), "+v"(nxt.z), "+v"(nxt.w));
+                    });
+#else
                     const U4 nxt = p + 8 <= plies ? philox4(rng.seed, id, ((ply0 + (uint64_t)p) >> 2) + 1, RNG_ACTION)
                                                   : cur;
-                    ply(p, cur.x);
-                    ply(p + 1, cur.y);
-                    ply(p + 2, cur.z);
-                    ply(p + 3, cur.w);
+                    ply(p, cur.x, nofill);
+#endif
+                    ply(p + 1, cur.y, nofill);
+                    ply(p + 2, cur.z, nofill);
+                    ply(p + 3, cur.w, nofill);
                     cur = nxt;
                     p += 4;
                 }
             }
             while (p < plies) {
                 const uint64_t g = ply0 + (uint64_t)p;
-                ply(p, pick4(philox4(rng.seed, id, g >> 2, RNG_ACTION), (uint32_t)(g & 3)));
+                ply(p, pick4(philox4(rng.seed, id, g >> 2, RNG_ACTION), (uint32_t)(g & 3)), nofill);
                 ++p;
             }
 #else
@@ -1621,13 +1643,13 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
                 const uint64_t g = ply0 + (uint64_t)p;
                 const U4 d4 = philox4(rng.seed, id, g >> 2, RNG_ACTION);
                 if ((g & 3) == 0 && p + 4 <= plies) {
-                    ply(p, d4.x);
-                    ply(p + 1, d4.y);
-                    ply(p + 2, d4.z);
-                    ply(p + 3, d4.w);
+                    ply(p, d4.x, nofill);
+                    ply(p + 1, d4.y, nofill);
+                    ply(p + 2, d4.z, nofill);
+                    ply(p + 3, d4.w, nofill);
                     p += 4;
                 } else {
-                    ply(p, pick4(d4, (uint32_t)(g & 3)));
+                    ply(p, pick4(d4, (uint32_t)(g & 3)), nofill);
                     ++p;
                 }
             }

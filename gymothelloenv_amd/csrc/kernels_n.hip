@@ -64,16 +64,13 @@ void launch_k_play(int lanes_per_board, oth_env* env, int n_plies, int32_t* acti
                                    env->wdl, rng_of(env), ply0);
                 return;
             }
-            hipLaunchKernelGGL((k_play_rand<N>), grid, block, 0, st, env->boards, env->meta, env->legal, env->E,
-                               env->flags, n_plies, actions, rewards, dones, env->wdl, rng_of(env), ply0);
+            launch_play_rand<N, OTH_POLICY_RANDOM>(env, n_plies, actions, rewards, dones, ply0, st);  // play_rand_n.hip
             return;
         }
     }
     if constexpr (OTH_FAST_GREEDY && POL == OTH_POLICY_GREEDY && std::is_same<Eng, Fills<N>>::value) {
         if (actions && rewards && dones && (env->flags & OTH_AUTO_RESET)) {
-            hipLaunchKernelGGL((k_play_rand<N, OTH_POLICY_GREEDY>), grid, block, 0, st, env->boards, env->meta,
-                               env->legal, env->E, env->flags, n_plies, actions, rewards, dones, env->wdl,
-                               rng_of(env), ply0);
+            launch_play_rand<N, OTH_POLICY_GREEDY>(env, n_plies, actions, rewards, dones, ply0, st);  // play_rand_n.hip
             return;
         }
     }
