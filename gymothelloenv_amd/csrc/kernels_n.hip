@@ -229,9 +229,31 @@ int launch_legal_moves(int n, const uint64_t* mover, const uint64_t* opp, uint64
 
 template <int N, typename T>
 void launch_observe_q(oth_env* env, int layout, uint32_t quads, void* out, hipStream_t st) {
+    T* o = static_cast<T*>(out);
+    if (OTH_OBS_WAVE) {  // one wave per 64 boards (k_observe_w)
+        const dim3 gw(grid_for(((long long)env->E + 63) / 64 * 64));
+        switch (layout) {
+            case OTH_OBS_BOARD:
+                hipLaunchKernelGGL((k_observe_w<N, OTH_OBS_BOARD, T>), gw, dim3(BLOCK), 0, st, env->boards, env->meta,
+                                   env->legal, env->E, o);
+                break;
+            case OTH_OBS_BOARD_LEGAL:
+                hipLaunchKernelGGL((k_observe_w<N, OTH_OBS_BOARD_LEGAL, T>), gw, dim3(BLOCK), 0, st, env->boards,
+                                   env->meta, env->legal, env->E, o);
+                break;
+            case OTH_OBS_MAKE_STATE:
+                hipLaunchKernelGGL((k_observe_w<N, OTH_OBS_MAKE_STATE, T>), gw, dim3(BLOCK), 0, st, env->boards,
+                                   env->meta, env->legal, env->E, o);
+                break;
+            default:
+                hipLaunchKernelGGL((k_observe_w<N, OTH_OBS_ABSOLUTE, T>), gw, dim3(BLOCK), 0, st, env->boards,
+                                   env->meta, env->legal, env->E, o);
+                break;
+        }
+        return;
+    }
     int grid = grid_for(quads);
     if (grid > (1 << 20)) grid = 1 << 20;
-    T* o = static_cast<T*>(out);
     switch (layout) {
         case OTH_OBS_BOARD:
             hipLaunchKernelGGL((k_observe_q<N, OTH_OBS_BOARD, T>), dim3(grid), dim3(BLOCK), 0, st, env->boards,
