@@ -65,11 +65,15 @@ def fused_bytes_per_launch(E, W, plies, record=True):
 
 
 def cpu_threads():
-    """Host cores this process may use: the affinity set, capped by the job's
-    thread budget (OMP_NUM_THREADS is the box's CPU share)."""
+    """(threads to use, affinity cores, what capped it): every core of the
+    affinity set unless the job's thread budget is smaller --
+    on the GPU box OMP_NUM_THREADS is the lease's CPU share, while the affinity
+    set shows the whole host's cores."""
     n = len(os.sched_getaffinity(0))
     cap = os.environ.get("OMP_NUM_THREADS")
-    return max(1, min(n, int(cap))) if cap and cap.isdigit() else n
+    if cap and cap.isdigit() and 0 < int(cap) < n:
+        return int(cap), n, "OMP_NUM_THREADS=%s (the job's CPU share)" % cap
+    return n, n, None
 
 
 def cpu_model():
@@ -112,7 +116,9 @@ def cpu_baseline(seconds, board_size=8, threads=None):
         of othello.py:273-343 (the reference's algorithm).
     Both play random moves from the device's Philox stream with auto-reset."""
     from oracle import oracle
-    T = threads or cpu_threads()
+    oracle.lib(), oracle.bb_lib()  # loaded (and rebuilt if stale) before any timing
+    T, affinity, capped_by = cpu_threads()
+    T = threads or T
     wall = max(2.0, seconds / T)
     flags = oracle.F_SUDDEN_DEATH | oracle.F_AUTO_RESET
     E, chunk = 1024, 16
@@ -135,6 +141,7 @@ def cpu_baseline(seconds, board_size=8, threads=None):
     sc_steps, sc_dt = _timed_threads(T, wall, scalar_work)
     model = cpu_model()
     return {"value": bb_steps / bb_dt, "unit": "env-steps/s", "cores": T, "kind": "port",
+            "affinity_cores": affinity, "cores_capped_by": capped_by,
             "per_core": bb_steps / bb_dt / T, "cpu_model": model,
             "sample": "%d threads x %d boards of random play, %dx%d, auto-reset, %d env-steps in %.1f s on %s: "
                       "oracle/cpu_bitboard.cpp (bitboard.hpp's shift/mask rules compiled for the host, g++ -O3), "
@@ -216,9 +223,25 @@ def spawn(argv, n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
-    rcs = [p.wait() for p in procs]
-    bad = [rc for rc in rcs if rc != 0]
-    return bad[0] if bad else 0
+    # poll every rank: one that dies makes the survivors wait in a collective
+    # until its timeout, so end them at once and report the failure
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = [rc for rc in rcs if rc not in (None, 0)]
+        if bad:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            return bad[0]
+        if all(rc == 0 for rc in rcs):
+            return 0
+        time.sleep(0.2)
 
 
 def main(argv=None):
@@ -242,6 +265,7 @@ def main(argv=None):
     # GPU), OTH_BENCH_DEVICE pins every rank to one device
     backend = os.environ.get("OTH_BENCH_BACKEND", "nccl")
     gpu = int(os.environ.get("OTH_BENCH_DEVICE", local))
+    shared = "OTH_BENCH_DEVICE" in os.environ and world > 1  # every rank on one device (a rehearsal)
     if args.dry_run:
         if world > 1:
             dist.init_process_group("gloo")
@@ -253,8 +277,10 @@ def main(argv=None):
         else:
             rows = [[rank, base, E]]
         if rank == 0:
-            print(json.dumps({"dry_run": True, "world": world, "global_envs": G, "plies_per_step": P,
-                              "shards": rows}), flush=True)
+            rec = make_record(args, world, G, E, P, args.board_size, not args.no_record, None, None, None,
+                              shared_device=shared, pmc={})
+            rec.update({"dry_run": True, "world": world, "global_envs": G, "plies_per_step": P, "shards": rows})
+            print(json.dumps(rec), flush=True)
         return 0
     if world > 1:
         if backend == "nccl":
@@ -284,11 +310,34 @@ def main(argv=None):
 
     run(args.warmup)
     env.counts(reset=True)
+    stream = torch.cuda.current_stream(dev)
+    solo = None
+    if world > 1:
+        # rank 0's shard timed alone on a twin handle while the other ranks wait
+        # (the same-shard one-GPU reference of the scaling curve; the twin keeps
+        # the measured handles' games, and so the W/D/L, independent of it)
+        torch.cuda.synchronize()
+        dist.barrier()
+        if rank == 0:
+            twin = ShardedVecOthelloEnv(G, rank=rank, world=world, board_size=n, auto_reset=True, seed=0,
+                                        initial_rand_steps=10 if args.policy == "greedy" else 0, device=dev)
+            twin.reset()
+            for _ in range(args.warmup):
+                twin.step_policy(args.policy, n_plies=P, actions=acts, rewards=rews, dones=dns, record=record)
+            torch.cuda.synchronize()
+            s0 = time.perf_counter()
+            for _ in range(args.steps):
+                twin.step_policy(args.policy, n_plies=P, actions=acts, rewards=rews, dones=dns, record=record)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - s0
+            solo = {"value": E * P * args.steps / dt, "unit": "env-steps/s", "boards": E,
+                    "ms_per_step": dt / args.steps * 1e3, "note": "rank 0's shard alone, other ranks idle"}
+            twin.close()
+        dist.barrier()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    stream = torch.cuda.current_stream(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
@@ -315,59 +364,8 @@ def main(argv=None):
         side = side_measurements(env.env, args.policy, E, n, W, dev, stream)
 
     if rank == 0:
-        env_steps = G * P * args.steps
-        avg_launch_s = kern_ms / 1e3 / args.steps
-        bps = step_bytes(W)
-        alg_launch = E * P * bps
-        achieved = alg_launch / avg_launch_s / 1e9
-        workload = "%s-play-%dx%d-E%d-P%d" % (args.policy, n, n, E, P)
-        if not record:
-            workload += "-norecord"
-        pmc = load_pmc(workload)
-        valu = None
-        if pmc and pmc.get("valu_insts_per_launch"):
-            rate = pmc["valu_insts_per_launch"] / avg_launch_s
-            valu = {"achieved_wave_insts_per_s": rate, "peak_wave_insts_per_s": VALU_PEAK_WAVE_INSTS,
-                    "frac": rate / VALU_PEAK_WAVE_INSTS,
-                    "insts_per_board_ply": pmc["valu_insts_per_launch"] / (E * P),
-                    "source": "SQ_INSTS_VALU per launch from profiles/pmc_traffic.json, this run's launch time"}
-        if args.policy == "random":
-            metric = METRIC
-        else:
-            metric = "env-steps/sec (%s policy on device, %dx%d)" % (args.policy, n, n)
-        config_name = "config2" if (world == 1 and G == CONFIG2_BOARDS) else \
-            ("config4" if (world == 8 and G == 8 * CONFIG4_BOARDS_PER_GPU) else "custom")
-        out = {
-            "metric": metric,
-            "value": env_steps / wall_max,
-            "unit": "env-steps/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": wall_max / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u64",
-            "data": "synthetic (standard opening, Philox random play, auto-reset)",
-            "config": {"workload": workload, "baseline_config": config_name, "boards_per_gpu": E,
-                       "global_boards": G, "board_size": n, "plies_per_step": P,
-                       "env_steps_per_step": G * P, "policy": args.policy, "per_ply_outputs_stored": record,
-                       "parallelism": "dp%d (independent shards, W/D/L all-gather only)" % world},
-            "roofline": {"bound": "valu-issue", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBPS,
-                         "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
-                         "kernel": play_kernel_name(n, args.policy, record), "avg_launch_us": avg_launch_s * 1e6,
-                         "launches_timed": args.steps,
-                         "algorithmic_bytes_per_env_step": bps,
-                         "algorithmic_bytes_per_launch": alg_launch,
-                         "fused_bytes_per_launch": fused_bytes_per_launch(E, W, P, record),
-                         "valu": valu,
-                         "note": "achieved/frac: SURVEY §8(d) bytes (40W+11 per env-step); traffic: PMC "
-                                 "FETCH_SIZE x2 + WRITE_SIZE per launch (the fused kernel keeps boards in "
-                                 "registers between plies); the limiter is integer VALU issue"},
-            "wdl": {"black_wins": wdl_total[0], "draws": wdl_total[1], "white_wins": wdl_total[2]},
-        }
+        out = make_record(args, world, G, E, P, n, record, wall_max, kern_ms, wdl_total, solo=solo,
+                          shared_device=shared)
         out.update(side)
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, n)
@@ -378,30 +376,186 @@ def main(argv=None):
     return 0
 
 
+def make_record(args, world, G, E, P, n, record, wall_max, kern_ms, wdl_total, solo=None, shared_device=False,
+                pmc=None):
+    """The JSON line rank 0 prints.  wall_max: max over ranks of the timed
+    region's wall time (s); kern_ms: rank 0's HIP-event time of the K launches
+    (None in --dry-run, which prints the same keys with null numbers)."""
+    from gymothelloenv_amd.vec_env import nwords
+    W = nwords(n)
+    env_steps = G * P * args.steps
+    bps = step_bytes(W)
+    alg_launch = E * P * bps
+    avg_launch_s = kern_ms / 1e3 / args.steps if kern_ms else None
+    achieved = alg_launch / avg_launch_s / 1e9 if avg_launch_s else None
+    workload = "%s-play-%dx%d-E%d-P%d" % (args.policy, n, n, E, P)
+    if not record:
+        workload += "-norecord"
+    pmc = pmc if pmc is not None else load_pmc(workload)
+    valu = None
+    if pmc and pmc.get("valu_insts_per_launch") and avg_launch_s:
+        rate = pmc["valu_insts_per_launch"] / avg_launch_s
+        valu = {"achieved_wave_insts_per_s": rate, "peak_wave_insts_per_s": VALU_PEAK_WAVE_INSTS,
+                "frac": rate / VALU_PEAK_WAVE_INSTS,
+                # SQ_INSTS_VALU counts wave-instructions, each serving 64 boards: x 64 / board-plies
+                # is the length of one board's (one lane's) VALU instruction stream per ply
+                "valu_insts_per_board_ply": pmc["valu_insts_per_launch"] * 64 / (E * P),
+                "wave_insts_per_launch": pmc["valu_insts_per_launch"],
+                "source": "SQ_INSTS_VALU per launch from %s, this run's launch time" % pmc.get("source", "?")}
+    metric = METRIC if args.policy == "random" else "env-steps/sec (%s policy on device, %dx%d)" % (args.policy, n, n)
+    config_name = "config2" if (world == 1 and G == CONFIG2_BOARDS) else \
+        ("config4" if (world == 8 and G == 8 * CONFIG4_BOARDS_PER_GPU) else "custom")
+    value = env_steps / wall_max if wall_max else None
+    out = {
+        "metric": metric,
+        "value": value,
+        "unit": "env-steps/s",
+        "n_gpus": 1 if shared_device else world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": wall_max / args.steps * 1e3 if wall_max else None,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic (standard opening, Philox random play, auto-reset)",
+        "config": {"workload": workload, "baseline_config": config_name, "boards_per_gpu": E,
+                   "global_boards": G, "board_size": n, "plies_per_step": P,
+                   "env_steps_per_step": G * P, "policy": args.policy, "per_ply_outputs_stored": record,
+                   "parallelism": "dp%d (independent shards, W/D/L all-gather only)" % world},
+        "roofline": {"bound": "hbm", "limiter": "integer VALU issue (see valu)",
+                     "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBPS if achieved else None,
+                     "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
+                     "traffic_source": pmc.get("source") if pmc else None,
+                     "kernel": play_kernel_name(n, args.policy, record),
+                     "avg_launch_us": avg_launch_s * 1e6 if avg_launch_s else None,
+                     "launches_timed": args.steps,
+                     "algorithmic_bytes_per_env_step": bps,
+                     "algorithmic_bytes_per_launch": alg_launch,
+                     "fused_bytes_per_launch": fused_bytes_per_launch(E, W, P, record),
+                     "valu": valu,
+                     "note": "achieved/frac: SURVEY §8(d) bytes (40W+11 per env-step) over the launch time; "
+                             "traffic: PMC FETCH_SIZE x2 + WRITE_SIZE per launch of the final build (the fused "
+                             "kernel keeps boards in registers between plies); the limiter is integer VALU issue"},
+        "wdl": {"black_wins": wdl_total[0], "draws": wdl_total[1], "white_wins": wdl_total[2]}
+        if wdl_total is not None else None,
+    }
+    if world > 1 or shared_device:
+        # SCALE reading aid: N > 1 runs config 4's 131,072 boards per GPU (two waves per SIMD),
+        # N = 1 config 2's 65,536 (one wave per SIMD), so compare per_gpu_value with
+        # single_gpu_same_shard (rank 0's shard timed alone, the other ranks idle at a barrier)
+        out["per_gpu_value"] = value / world if value else None
+        out["single_gpu_same_shard"] = solo
+        out["ranks"] = world
+        out["shared_device"] = bool(shared_device)
+    return out
+
+
+def _time_launches(stream, fn, k):
+    """Average time of k back-to-back launches fn(i) on `stream` (HIP events)."""
+    import torch
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(stream)
+    for i in range(k):
+        fn(i)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / k
+
+
+def step_external(E, n, dev, stream, plies=64):
+    """oth_step (OthelloBaseEnv.step, othello.py:412-462) with external device
+    actions, one launch per ply (the north star's step(action) path: the state
+    round-trips HBM every ply).  The actions are P plies of recorded on-device
+    random play (all legal, auto-reset), replayed from the recording's start
+    state; the replay must end in the recording's state (checked)."""
+    import torch
+
+    from gymothelloenv_amd import VecOthelloEnv
+    from gymothelloenv_amd.vec_env import nwords
+    W = nwords(n)
+    env = VecOthelloEnv(E, board_size=n, auto_reset=True, seed=7, device=dev)
+    env.step_policy("random", n_plies=30, record=False)  # a mid-game mix of boards
+    b0, m0, l0 = env.get_state()
+    ply0 = env.ply_counter
+    acts = torch.empty(plies, E, dtype=torch.int32, device=dev)
+    rec_r = torch.empty(plies, E, dtype=torch.int32, device=dev)
+    rec_d = torch.empty(plies, E, dtype=torch.uint8, device=dev)
+    env.step_policy("random", n_plies=plies, actions=acts, rewards=rec_r, dones=rec_d)
+    b1, m1, l1 = env.get_state()
+    rew = torch.empty(E, dtype=torch.int32, device=dev)
+    don = torch.empty(E, dtype=torch.uint8, device=dev)
+
+    def replay(i):
+        env.step(acts[i], rewards=rew, dones=don, observe=False)
+
+    def matches():
+        b2, m2, l2 = env.get_state()
+        return bool(torch.equal(b1, b2) and torch.equal(m1, m2) and torch.equal(l1, l2) and
+                    torch.equal(rew, rec_r[-1]) and torch.equal(don, rec_d[-1]))
+    eager_us = None
+    for _ in range(2):  # eager launches (host launch path included); the first warms up
+        env.set_state(b0, m0, l0)
+        env.ply_counter = ply0
+        eager_us = _time_launches(stream, replay, plies)
+    same = matches()
+    # the same P launches replayed from a HIP graph: the kernels back to back, no host in the loop
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g), env.graph_region():
+        for i in range(plies):
+            replay(i)
+    us = None
+    for _ in range(2):
+        env.set_state(b0, m0, l0)
+        us = _time_launches(stream, lambda i: g.replay(), 1) / plies
+    same = same and matches()
+    env.close()
+    bps = step_bytes(W)
+    gbs = E * bps / (us * 1e-6) / 1e9
+    return {"kernel": "k_ply_step<%d>" % n if W == 1 else "k_step<%d>" % n, "boards": E, "value": E / (us * 1e-6),
+            "unit": "env-steps/s", "avg_launch_us": us, "launches": plies,
+            "timing": "HIP graph of the %d launches, HIP events around the replay" % plies,
+            "eager_avg_launch_us": eager_us,
+            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": gbs / HBM_PEAK_GBPS, "algorithmic_bytes_per_env_step": bps},
+            "replay_equals_recording": same}
+
+
+def single_ply(env, policy, E, W, dev, stream, k=200):
+    """oth_step_policy with one ply per launch (k_ply_rand for random play on
+    one-word boards): every board's state through HBM every ply."""
+    import torch
+    a1 = torch.empty(1, E, dtype=torch.int32, device=dev)
+    r1 = torch.empty(1, E, dtype=torch.int32, device=dev)
+    d1 = torch.empty(1, E, dtype=torch.uint8, device=dev)
+    for _ in range(20):
+        env.step_policy(policy, n_plies=1, actions=a1, rewards=r1, dones=d1)
+    us = _time_launches(stream, lambda i: env.step_policy(policy, n_plies=1, actions=a1, rewards=r1, dones=d1), k)
+    gbs = E * step_bytes(W) / (us * 1e-6) / 1e9
+    return {"boards": E, "value": E / (us * 1e-6), "unit": "env-steps/s", "avg_launch_us": us, "launches": k,
+            "algorithmic_GBps": gbs, "frac": gbs / HBM_PEAK_GBPS}
+
+
 def side_measurements(env, policy, E, n, W, dev, stream):
-    """Beside the headline (never `value`): one ply per launch (the north-star
-    per-step shape: state through HBM every ply) and the learners' masked
+    """Beside the headline (never `value`): the per-step paths with the state
+    through HBM every ply -- oth_step with external actions (`step_external`)
+    and one-ply launches of the policy (`single_ply_launches`) -- at config 2's
+    65,536 boards and config 4's 1,048,576 on one GPU, and the learners' masked
     categorical over 4,194,304 boards' fp32 logits (beyond the 256 MiB MALL)."""
     import ctypes
 
     import torch
-    out = {}
-    a1 = torch.empty(1, E, dtype=torch.int32, device=dev)
-    r1 = torch.empty(1, E, dtype=torch.int32, device=dev)
-    d1 = torch.empty(1, E, dtype=torch.uint8, device=dev)
-    for _ in range(50):
-        env.step_policy(policy, n_plies=1, actions=a1, rewards=r1, dones=d1)
-    torch.cuda.synchronize()
-    k1 = 500
+
+    from gymothelloenv_amd import VecOthelloEnv
+    out = {"step_external": [step_external(Eb, n, dev, stream) for Eb in (E, 1048576)]}
+    big = VecOthelloEnv(1048576, board_size=n, auto_reset=True, seed=0, device=dev)
+    big.step_policy(policy, n_plies=20, record=False)
+    out["single_ply_launches"] = [single_ply(env, policy, E, W, dev, stream),
+                                  single_ply(big, policy, 1048576, W, dev, stream, k=100)]
+    big.close()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for _ in range(k1):
-        env.step_policy(policy, n_plies=1, actions=a1, rewards=r1, dones=d1)
-    e1.record(stream)
-    torch.cuda.synchronize()
-    us = e0.elapsed_time(e1) * 1e3 / k1
-    out["single_ply_launches"] = {"value": E / (us * 1e-6), "unit": "env-steps/s", "avg_launch_us": us,
-                                  "algorithmic_GBps": E * step_bytes(W) / (us * 1e-6) / 1e9, "launches": k1}
 
     Em, nn = 4194304, n * n
     g = torch.Generator(device=dev).manual_seed(0)

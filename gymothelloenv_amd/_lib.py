@@ -22,6 +22,11 @@ OTH_POLICY_GREEDY = 1
 OTH_POLICY_MAXIMIN1 = 2
 OTH_POLICY_MAXIMIN2 = 3
 OTH_POLICY_MAXIMIN3 = 4
+OTH_MAXIMIN_MAX_DEPTH = 10
+
+
+def OTH_POLICY_MAXIMIN(d):
+    return OTH_POLICY_MAXIMIN1 + int(d) - 1
 OTH_OBS_BOARD = 0
 OTH_OBS_BOARD_LEGAL = 1
 OTH_OBS_MAKE_STATE = 2
@@ -62,6 +67,7 @@ SIGNATURES = {
     "oth_graph_begin": (_I32, [_P, _P]),
     "oth_graph_end": (_I32, [_P, _U64, _I32, _P, _P]),
     "oth_graph_offsets": (_I32, [_P, _I32, _P]),
+    "oth_graph_release": (_I32, [_P, _I32]),
     "oth_shape": (_I32, [_P, _P, _P, _P]),
     "oth_last_error": (ctypes.c_char_p, []),
     "oth_version": (ctypes.c_char_p, []),

@@ -149,67 +149,10 @@ OTH_HD int popcount(const BB<W>& a) {
     return c;
 }
 
-#ifndef OTH_SHIFT32
-#define OTH_SHIFT32 0
-#endif
-
-#if defined(__HIP_DEVICE_COMPILE__)
-// ({hi, lo} >> c)[31:0]: one full-rate VALU op (v_alignbit_b32)
-__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t c) {
-    return __builtin_amdgcn_alignbit(hi, lo, c);
-}
-#endif
 
 // Logical shift of the whole W-word board by S bits (S > 0 toward higher squares).
 template <int W, int S>
 OTH_HD BB<W> shift(const BB<W>& x) {
-#if defined(__HIP_DEVICE_COMPILE__) && OTH_SHIFT32
-    // On the device the board is handled as 2W dwords: each output dword is one
-    // funnel shift of two input dwords (v_alignbit_b32), instead of 64-bit
-    // shifts (v_lshlrev_b64 / v_lshrrev_b64) plus or-combines.
-    if constexpr (S != 0) {
-        constexpr int D = 2 * W;
-        uint32_t v[D], r[D];
-#pragma unroll
-        for (int i = 0; i < W; ++i) {
-            v[2 * i] = (uint32_t)x.w[i];
-            v[2 * i + 1] = (uint32_t)(x.w[i] >> 32);
-        }
-        if constexpr (S > 0) {
-            constexpr int q = S / 32, s = S % 32;
-#pragma unroll
-            for (int i = 0; i < D; ++i) {
-                if (i - q < 0) {
-                    r[i] = 0;
-                } else if (s == 0) {
-                    r[i] = v[i - q];
-                } else if (i - q - 1 < 0) {
-                    r[i] = v[i - q] << s;
-                } else {
-                    r[i] = funnel(v[i - q], v[i - q - 1], 32 - s);
-                }
-            }
-        } else {
-            constexpr int T = -S, q = T / 32, s = T % 32;
-#pragma unroll
-            for (int i = 0; i < D; ++i) {
-                if (i + q >= D) {
-                    r[i] = 0;
-                } else if (s == 0) {
-                    r[i] = v[i + q];
-                } else if (i + q + 1 >= D) {
-                    r[i] = v[i + q] >> s;
-                } else {
-                    r[i] = funnel(v[i + q + 1], v[i + q], s);
-                }
-            }
-        }
-        BB<W> out;
-#pragma unroll
-        for (int i = 0; i < W; ++i) out.w[i] = ((uint64_t)r[2 * i + 1] << 32) | r[2 * i];
-        return out;
-    }
-#endif
     if constexpr (S == 0) {
         return x;
     } else if constexpr (S > 0) {
@@ -321,9 +264,6 @@ OTH_HD uint64_t maj3_64(uint64_t a, uint64_t b, uint64_t c) {
     return (a & b) | (c & (a | b));
 #endif
 }
-#ifndef OTH_GREEDY_MASKSEL
-#define OTH_GREEDY_MASKSEL 0  // OneWord::greedy's plane narrowing with mask arithmetic instead of a select
-#endif
 
 template <int N>
 struct Geo {
@@ -364,30 +304,10 @@ struct Geo {
 #define OTH_PROP_REUSE 1  // last doubling step reuses the previous propagator where it covers N - 2
 #endif
 
-#ifndef OTH_ANDOR
-#define OTH_ANDOR 0
-#endif
-
-// (a & b) | c.  hipcc does not fuse 64-bit and/or pairs into v_and_or_b32
-// (it does for 32-bit values), so on the device each 32-bit half is one
-// explicit v_and_or_b32: 2 VALU ops per word instead of 4.
+// (a & b) | c (the multi-word Kogge-Stone step; one-word and dword scans use U2 / DW)
 template <int W>
 OTH_HD BB<W> and_or(const BB<W>& a, const BB<W>& b, const BB<W>& c) {
-#if defined(__HIP_DEVICE_COMPILE__) && OTH_ANDOR
-    BB<W> r;
-#pragma unroll
-    for (int i = 0; i < W; ++i) {
-        uint32_t lo, hi;
-        asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(lo) : "v"((uint32_t)a.w[i]), "v"((uint32_t)b.w[i]),
-            "v"((uint32_t)c.w[i]));
-        asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(hi) : "v"((uint32_t)(a.w[i] >> 32)),
-            "v"((uint32_t)(b.w[i] >> 32)), "v"((uint32_t)(c.w[i] >> 32)));
-        r.w[i] = ((uint64_t)hi << 32) | lo;
-    }
-    return r;
-#else
     return (a & b) | c;
-#endif
 }
 
 // Propagators of one direction for the discs O: pro[k] holds the squares x with
@@ -1049,12 +969,7 @@ struct OneWord {
 #pragma unroll
         for (int i = 4; i >= 0; --i) {
             const uint64_t h = cand & to64(tot[i]);
-#if OTH_GREEDY_MASKSEL
-            const uint64_t keep = (uint64_t)(h == 0ull) - 1ull;  // all ones when h != 0
-            cand = (h & keep) | (cand & ~keep);
-#else
             cand = h ? h : cand;
-#endif
         }
         return cand ? __builtin_ctzll(cand) : -1;
     }

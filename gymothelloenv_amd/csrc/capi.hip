@@ -161,14 +161,16 @@ int oth_create(int32_t n_envs, int32_t board_size, uint32_t flags, uint64_t seed
     const size_t ctr_bytes = (size_t)OTH_GRAPH_SLOTS * 2 * sizeof(uint64_t);
     if (err == hipSuccess) err = hipMalloc((void**)&env->ctr_slots, ctr_bytes);
     if (err == hipSuccess) err = hipMemset(env->ctr_slots, 0, ctr_bytes);
+    if (err == hipSuccess && env->W == 1) err = hipMalloc((void**)&env->rays, 8 * 64 * sizeof(uint64_t));
     env->cur_off = env->ctr_slots;
     env->graph_slot = 0;
-    env->next_slot = 1;
+    env->slots_used = 1;
     if (err != hipSuccess) {
         oth_destroy(env);
         return hip_fail(err, "oth_create: allocation");
     }
-    int rc = oth_reset(env, nullptr, nullptr);
+    int rc = with_n(n, [&](auto NC) { return launch_fill_rays<decltype(NC)::value>(env, nullptr); });
+    if (rc == OTH_OK) rc = oth_reset(env, nullptr, nullptr);
     if (rc == OTH_OK) {
         err = hipStreamSynchronize(nullptr);
         if (err != hipSuccess) rc = hip_fail(err, "oth_create: reset");
@@ -190,6 +192,7 @@ int oth_destroy(oth_env* env) {
     if (env->wdl) (void)hipFree(env->wdl);
     if (env->wdl_vs) (void)hipFree(env->wdl_vs);
     if (env->ctr_slots) (void)hipFree(env->ctr_slots);
+    if (env->rays) (void)hipFree(env->rays);
     delete env;
     return OTH_OK;
 }
@@ -212,7 +215,7 @@ int oth_step_policy(oth_env* env, int32_t policy, int32_t n_plies, int32_t* acti
                     uint8_t* dones, oth_stream_t stream) {
     OTH_CHECK_ENV(env);
     if (n_plies < 0) return fail(OTH_EINVAL, "n_plies must be >= 0");
-    if (policy < OTH_POLICY_RANDOM || policy > OTH_POLICY_MAXIMIN3) return fail(OTH_EINVAL, "unknown policy");
+    if (policy < OTH_POLICY_RANDOM || policy > OTH_POLICY_LAST) return fail(OTH_EINVAL, "unknown policy");
     if (n_plies == 0) return OTH_OK;
     const uint64_t ply0 = env->ply;
     env->ply += (uint64_t)n_plies;
@@ -225,7 +228,7 @@ int oth_step_policy(oth_env* env, int32_t policy, int32_t n_plies, int32_t* acti
 int oth_reset_vs(oth_env* env, int32_t opponent_policy, const int8_t* protagonist, const uint8_t* mask,
                  oth_stream_t stream) {
     OTH_CHECK_ENV(env);
-    if (opponent_policy < OTH_POLICY_RANDOM || opponent_policy > OTH_POLICY_MAXIMIN3)
+    if (opponent_policy < OTH_POLICY_RANDOM || opponent_policy > OTH_POLICY_LAST)
         return fail(OTH_EINVAL, "unknown opponent policy");
     const uint64_t call = env->ply++;
     return with_n(env->n, [&](auto NC) {
@@ -238,7 +241,7 @@ int oth_step_vs(oth_env* env, int32_t opponent_policy, const int32_t* actions, c
                 int32_t* rewards, uint8_t* dones, int32_t* plies, oth_stream_t stream) {
     OTH_CHECK_ENV(env);
     if (!actions) return fail(OTH_EINVAL, "actions is NULL");
-    if (opponent_policy < OTH_POLICY_RANDOM || opponent_policy > OTH_POLICY_MAXIMIN3)
+    if (opponent_policy < OTH_POLICY_RANDOM || opponent_policy > OTH_POLICY_LAST)
         return fail(OTH_EINVAL, "unknown opponent policy");
     const uint64_t call = env->ply++;
     return with_n(env->n, [&](auto NC) {
@@ -250,8 +253,8 @@ int oth_step_vs(oth_env* env, int32_t opponent_policy, const int32_t* actions, c
 int oth_policy_actions(oth_env* env, int32_t policy, int32_t* out, oth_stream_t stream) {
     OTH_CHECK_ENV(env);
     if (!out) return fail(OTH_EINVAL, "out is NULL");
-    if (policy < OTH_POLICY_GREEDY || policy > OTH_POLICY_MAXIMIN3)
-        return fail(OTH_EINVAL, "policy must be greedy or maximin");
+    if (policy < OTH_POLICY_GREEDY || policy > OTH_POLICY_LAST)
+        return fail(OTH_EINVAL, "policy must be greedy or maximin (depth 1 .. OTH_MAXIMIN_MAX_DEPTH)");
     return with_n(env->n, [&](auto NC) {
         return launch_policy_actions<decltype(NC)::value>(env, policy, out, (hipStream_t)stream);
     });
@@ -332,8 +335,10 @@ __global__ void k_graph_advance(uint64_t* __restrict__ off, uint64_t d_ply, uint
 int oth_graph_begin(oth_env* env, int32_t* slot) {
     if (!env || !slot) return fail(OTH_EINVAL, "NULL argument");
     if (env->graph_slot) return fail(OTH_EINVAL, "a graph region is already open on this handle");
-    if (env->next_slot >= OTH_GRAPH_SLOTS) return fail(OTH_EINVAL, "no graph counter slot left on this handle");
-    const int k = env->next_slot++;
+    if (env->slots_used == ~0ull)
+        return fail(OTH_EINVAL, "no graph counter slot left on this handle (oth_graph_release frees one)");
+    const int k = __builtin_ctzll(~env->slots_used);  // the lowest free slot
+    env->slots_used |= 1ull << k;
     env->graph_slot = k;
     env->ply_saved = env->ply;
     env->ply = (uint64_t)k << OTH_GRAPH_COUNTER_SHIFT;
@@ -356,6 +361,17 @@ int oth_graph_end(oth_env* env, uint64_t d_sample, int32_t enqueue, uint64_t* d_
     hipLaunchKernelGGL(k_graph_advance, dim3(1), dim3(64), 0, (hipStream_t)stream, env->ctr_slots + 2 * k, dp,
                        d_sample);
     return oth_host::after_launch("oth_graph_end");
+}
+
+// A released slot keeps its device offsets: a later region on it draws past
+// every counter the earlier graph drew, so ranges stay disjoint even if that
+// graph is still replayed.
+int oth_graph_release(oth_env* env, int32_t slot) {
+    if (!env) return fail(OTH_EINVAL, "NULL oth_env");
+    if (slot <= 0 || slot >= OTH_GRAPH_SLOTS) return fail(OTH_EINVAL, "slot out of range");
+    if (slot == env->graph_slot) return fail(OTH_EINVAL, "the slot's graph region is still open");
+    env->slots_used &= ~(1ull << slot);
+    return OTH_OK;
 }
 
 int oth_graph_offsets(const oth_env* env, int32_t slot, uint64_t* out) {

@@ -30,9 +30,6 @@
 
 using namespace oth;
 
-#ifndef OTH_DUO
-#define OTH_DUO 0  // 1: Duo engine (two lanes per board, split axes + rays) for random play, N <= 8
-#endif
 #ifndef OTH_FILLS
 #define OTH_FILLS 1  // Fills engine (ray tables + the legal scan's fills) for random play, N <= 8
 #endif
@@ -96,9 +93,6 @@ using namespace oth;
 #ifndef OTH_RAND_PIPE
 #define OTH_RAND_PIPE 1  // k_play_rand: the next Philox block computed inside the current 4-ply group
 #endif
-#ifndef OTH_SS_STAGE
-#define OTH_SS_STAGE 0  // 1: k_sample_step stages the wave's logits rows through LDS (coalesced loads; measured slower: 8.6 -> 11.1 us per ply at 8x8)
-#endif
 #ifndef OTH_SS_PAIR
 #define OTH_SS_PAIR 1  // oth_sample_step on lane pairs for one-word boards (k_sample_step2)
 #endif
@@ -111,32 +105,14 @@ using namespace oth;
 #ifndef OTH_SS2_STAGE
 #define OTH_SS2_STAGE 1  // k_sample_step2 (8x8): the wave's logits rows through LDS, coalesced loads
 #endif
-#ifndef OTH_PLAY_PAIR
-#define OTH_PLAY_PAIR 0  // 1: k_play_rand on lane pairs (k_play_rand2, PairFills): bit-identical but 8x8 0.78 -> 0.98 us per ply (233 VALU per lane-ply vs 308 per board-ply; two waves reach 3.7 cycles per VALU per SIMD, one wave 5.5)
-#endif
 #ifndef OTH_SS_PAIR_W
 #define OTH_SS_PAIR_W 1  // oth_sample_step on lane pairs for two-word boards too (N = 9..11; Solo step on both lanes)
 #endif
 #ifndef OTH_SS_PAIR_W_MAX_E
 #define OTH_SS_PAIR_W_MAX_E 32768  // two-word boards whose rows are not float4-aligned: pairs up to this many boards
 #endif
-#ifndef OTH_SS2_SOLO
-#define OTH_SS2_SOLO 0  // k_sample_step2: step with Solo on each lane instead of Duo
-#endif
-#ifndef OTH_SS_ABL
-#define OTH_SS_ABL 0
-#endif
-#ifndef OTH_RAYS_REP
-#define OTH_RAYS_REP 0  // k_play_rand (N <= 8): flips from the lane-replicated ray table (FillsRep, conflict-free ds_read_b128)
-#endif
 #ifndef OTH_FLIP_TURN
 #define OTH_FLIP_TURN 2  // Fills::flip toward lower squares on the board turned by 180 degrees, no 64-bit clz (2: turned rays tabled under the unturned square, +3 % at 8x8; 1: addressed at NN-1-a, -1.5 %)
-#endif
-#ifndef OTH_DRAW_UNROLL
-#define OTH_DRAW_UNROLL 1  // k_play random: four plies unrolled per Philox block (no per-ply word rotation)
-#endif
-#ifndef OTH_DRAW_ROTATE
-#define OTH_DRAW_ROTATE 1  // k_play random: rotate the 4-word Philox block per ply instead of picking word g % 4
 #endif
 
 namespace oth_dev {
@@ -448,71 +424,6 @@ struct Fills {
     __device__ __forceinline__ bool leader() const { return true; }
 };
 
-// FillsRep<N> (k_play_rand, OTH_RAYS_REP): Fills whose flips read the ray
-// tables from 16 copies laid out so that every lane of a wave reads a 16-byte
-// slot of the LDS bank row of its own.  Entry (sq, k) holds the rays of
-// directions 2k, 2k+1 (k = 2, 3: the turned rays of 4..7, as OTH_FLIP_TURN 2)
-// at byte sq*1024 + k*256 + 16*(lane & 15): a flip is four ds_read_b128 with
-// immediate offsets, and the 16 lanes of each of ds_read_b128's lane groups
-// ({0-3,12-15,20-27}, ...) hit 16 distinct slots whatever squares they play:
-// conflict-free, 4 LDS cycles a read, against 8 plus the random squares' bank
-// conflicts for each ds_read2st64_b64 pair from the 4-KiB table.  64 KiB of
-// LDS per block (two 256-lane blocks per CU).
-constexpr int REP_ENTRIES = 64 * 4 * 16;
-template <int N>
-__device__ __forceinline__ void fill_rays_rep(ulonglong2* rep) {
-    static_assert(OTH_FLIP_TURN == 2, "the replicated table holds the turned rays");
-    for (int i = threadIdx.x; i < 64 * 4; i += BLOCK) {
-        const int sq = i >> 2, k = i & 3;
-        uint64_t r2[2] = {0, 0};
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int d = 2 * k + j;
-            if (sq < N * N) {
-                const int dr = __builtin_amdgcn_sbfe((int)0xFFF01110u, 4 * d, 4);
-                const int dc = __builtin_amdgcn_sbfe((int)0x1F0FF101u, 4 * d, 4);
-                int row = sq / N + dr, col = sq % N + dc;
-                while (row >= 0 && row < N && col >= 0 && col < N) {
-                    const int s2 = row * N + col;
-                    r2[j] |= 1ull << (d >= 4 ? N * N - 1 - s2 : s2);
-                    row += dr;
-                    col += dc;
-                }
-            }
-        }
-        ulonglong2 v;
-        v.x = r2[0];
-        v.y = r2[1];
-        // slot (s + i) & 15: eight consecutive threads write eight distinct slots
-#pragma unroll
-        for (int s = 0; s < 16; ++s) rep[i * 16 + ((s + i) & 15)] = v;
-    }
-    __syncthreads();
-}
-template <int N>
-struct FillsRep : Fills<N> {
-    const ulonglong2* rep;  // + (lane & 15)
-    __device__ __forceinline__ FillsRep(const uint64_t* lds, const ulonglong2* rp)
-        : Fills<N>(0, lds), rep(rp + (threadIdx.x & 15)) {}
-    __device__ __forceinline__ BB<1> flip(const BB<1>&, const BB<1>&, int a) const {
-        const ulonglong2* r = rep + a * 64;
-        const ulonglong2 v0 = r[0], v1 = r[16], v2 = r[32], v3 = r[48];
-        const uint64_t* t = this->t;
-        const uint64_t up[4] = {v0.x, v0.y, v1.x, v1.y}, dn[4] = {v2.x, v2.y, v3.x, v3.y};
-        uint64_t f = 0, g = 0;
-#pragma unroll
-        for (int d = 0; d < 4; ++d) f |= and3_64(up[d], t[d], (up[d] & ~t[d]) - 1ull);  // as Fills::flip
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-            const uint64_t tt = OneWord<N>::turn180(t[4 + d]);
-            g |= and3_64(dn[d], tt, (dn[d] & ~tt) - 1ull);
-        }
-        BB<1> out;
-        out.w[0] = f | OneWord<N>::turn180(g);
-        return out;
-    }
-};
-
 // FillsW<N>: the Fills engine for multi-word boards (N >= 9): the legal scan
 // keeps its eight fills (legal_moves_fills) and update_board's flips come from
 // them and a ray table of BB<W> entries in LDS (flips_fills), without the
@@ -736,9 +647,7 @@ __device__ __forceinline__ void finish_step(Lane<N>& s, bool tw, bool valid, con
         const BB<W> om = eng.legal(O, P);
         const bool opp_pass = !any(om);
         BB<W> nl = om;
-#ifndef OTH_ABLATE_NOPASS
         if (opp_pass) nl = eng.legal(P, O);
-#endif
         s.legal = nl;
         if (!opp_pass) {
             new_tw = !tw;
@@ -785,11 +694,7 @@ __device__ __forceinline__ void step_lane(Lane<N>& s, int a, uint32_t flags, int
     if constexpr (PICKED && Eng::RAY_WORDS > 0 && W == 1) {
         const bool valid = a >= 0;
         const uint64_t m = valid ? 1ull << (a & 63) : 0ull;
-#ifdef OTH_ABLATE_NOFLIP  // timing ablation only
-        const uint64_t f = 0;
-#else
         const uint64_t f = eng.flip(P, O, a & 63).w[0] & (0ull - (uint64_t)valid);
-#endif
         P.w[0] |= f | m;
         O.w[0] &= ~(f | m);
         finish_step<N>(s, tw, valid, P, O, flags, reward, done, winner, eng);
@@ -798,11 +703,7 @@ __device__ __forceinline__ void step_lane(Lane<N>& s, int a, uint32_t flags, int
     const bool valid = a >= 0 && a < NN && test(s.legal, a);  // `action not in possible_moves` (:417)
     if (valid) {                                               // update_board (:391-410)
         const BB<W> m = square<W>(a);
-#ifdef OTH_ABLATE_NOFLIP  // timing ablation only
-        const BB<W> f = zero<W>();
-#else
         const BB<W> f = eng.flip(P, O, a);
-#endif
         P |= f | m;
         O = O & ~(f | m);
     }
@@ -942,6 +843,81 @@ __device__ int maximin_node(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O, cons
     return best;
 }
 
+// MaxiMinPolicy(D).get_action for a runtime depth D (the OTH_POLICY_MAXIMIN_DEEP
+// launches, D >= 4; maximin_node's rules): the reference's recursion
+// (simple_policies.py:111-155) as a depth-first walk over an explicit stack,
+// one level per search depth -- level l moves the root's side at even l and
+// holds (mover, other, moves not yet tried, best value, move being tried).
+// The level above the leaves takes its value from the greedy planes' maximum
+// flip count, as maximin_node does.  -1 without a move (the reference's None).
+template <int N>
+__device__ int maximin_search(const BB<Geo<N>::W>& P0, const BB<Geo<N>::W>& O0, const BB<Geo<N>::W>& L0, int D) {
+    constexpr int W = Geo<N>::W;
+    constexpr int MAXD = OTH_MAXIMIN_MAX_DEPTH;
+    BB<W> SP[MAXD], SO[MAXD], SR[MAXD];
+    int SV[MAXD], SM[MAXD];
+    if (!any(L0)) return -1;
+    int best_move = -1, l = 0;
+    SP[0] = P0;
+    SO[0] = O0;
+    SR[0] = L0;
+    SV[0] = -1;
+    for (;;) {
+        if (!any(SR[l])) {  // every move of level l tried: its value goes to the level above
+            if (l == 0) break;
+            const int v = SV[l];
+            --l;
+            if ((l & 1) == 0 ? v > SV[l] : v < SV[l]) {  // np.argmax / np.argmin: the first of equals
+                SV[l] = v;
+                if (l == 0) best_move = SM[l];
+            }
+            continue;
+        }
+        // the lowest untried move of level l (possible_moves ascending)
+        BB<W> R = SR[l], m = zero<W>();
+        int b = -1;
+#pragma unroll
+        for (int i = W - 1; i >= 0; --i)
+            if (R.w[i]) b = 64 * i + ctz64(R.w[i]);
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+            m.w[i] = (b >> 6) == i ? 1ull << (b & 63) : 0ull;
+            R.w[i] &= ~m.w[i];
+        }
+        SR[l] = R;
+        SM[l] = b;
+        const BB<W> P = SP[l], O = SO[l];
+        const BB<W> f = flips<N>(P, O, m);
+        const BB<W> P2 = P | f | m;
+        const BB<W> O2 = O & ~(f | m);
+        const bool mine = (l & 1) == 0;
+        int v = popcount(mine ? P2 : O2);  // a leaf: my disc count (:117-126)
+        bool leaf = true;
+        if (l + 1 < D && any(~(P2 | O2) & Geo<N>::BOARD)) {
+            BB<W> t2[8];
+            const BB<W> L2 = legal_moves_fills<N>(O2, P2, t2);
+            if (any(L2)) {  // no reply: the game ends or the turn is forced back to a side without moves
+                if (l + 2 == D) {  // the child's moves end the search: its best from the planes
+                    const int mf = PlanesW<N>::max_flips(t2, L2);
+                    v = ((l + 1) & 1) == 0 ? popcount(O2) + 1 + mf : popcount(P2) - mf;
+                } else {
+                    ++l;
+                    SP[l] = O2;
+                    SO[l] = P2;
+                    SR[l] = L2;
+                    SV[l] = (l & 1) == 0 ? -1 : 0x7fffffff;
+                    leaf = false;
+                }
+            }
+        }
+        if (leaf && (mine ? v > SV[l] : v < SV[l])) {
+            SV[l] = v;
+            if (l == 0) best_move = b;
+        }
+    }
+    return best_move;
+}
+
 template <int N, int D>
 __device__ __forceinline__ int maximin_action(const Lane<N>& s) {
     const bool tw = (s.meta & M_TURN_WHITE) != 0;
@@ -950,15 +926,20 @@ __device__ __forceinline__ int maximin_action(const Lane<N>& s) {
     return move;
 }
 
-// The move of a deterministic scripted policy (everything but RANDOM).
+// The move of a deterministic scripted policy (everything but RANDOM); depth:
+// the search depth of OTH_POLICY_MAXIMIN_DEEP (Rng::depth).
+constexpr int OTH_POLICY_MAXIMIN_DEEP = 0x100;  // launcher-internal: MaxiMin of a runtime depth >= 4
 template <int N, int POLICY, typename Eng>
-__device__ __forceinline__ int policy_action(const Lane<N>& s, const Eng& eng) {
+__device__ __forceinline__ int policy_action(const Lane<N>& s, const Eng& eng, int depth = 0) {
     if constexpr (POLICY == OTH_POLICY_GREEDY) {
         return greedy_action<N>(s, eng);
     } else if constexpr (POLICY == OTH_POLICY_MAXIMIN2) {
         return maximin_action<N, 2>(s);
     } else if constexpr (POLICY == OTH_POLICY_MAXIMIN3) {
         return maximin_action<N, 3>(s);
+    } else if constexpr (POLICY == OTH_POLICY_MAXIMIN_DEEP) {
+        const bool tw = (s.meta & M_TURN_WHITE) != 0;
+        return maximin_search<N>(pick(tw, s.white, s.black), pick(tw, s.black, s.white), s.legal, depth);
     } else {
         return -1;
     }
@@ -1024,11 +1005,13 @@ __device__ __forceinline__ void tally(unsigned long long* wdl, uint32_t b, uint3
 #endif
 }
 
+// A launch's draw context (and the search depth of OTH_POLICY_MAXIMIN_DEEP launches).
 struct Rng {
     uint64_t seed;
     uint32_t id_base;
     int init_rand;
     const uint64_t* ply_off;  // device offset of the ply counter: slot 0 (= 0) eagerly, a graph region's slot under capture
+    int depth;                // MaxiMinPolicy(depth) for OTH_POLICY_MAXIMIN_DEEP (depth >= 4)
 };
 
 template <int N>
@@ -1057,9 +1040,10 @@ __global__ __launch_bounds__(BLOCK) void k_step(uint64_t* __restrict__ boards, u
     if (e < E) {
         Lane<N> s;
         load_lane<N>(s, boards, meta, legal, e);
+        const int a = actions[e];  // with the board's loads, not behind the terminated test
         const bool was_term = (s.meta & M_TERMINATED) != 0;
         int r, d, win;
-        step_lane<N>(s, actions[e], flags, r, d, win, Solo<N>(0, nullptr));
+        step_lane<N>(s, a, flags, r, d, win, Solo<N>(0, nullptr));
         if (d && !was_term) {
             cb = win == BLACK_DISK;
             cd = win == NO_DISK;
@@ -1111,14 +1095,10 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
                 const uint32_t rl = s.meta >> M_RAND_SHIFT;
                 if (POLICY == OTH_POLICY_RANDOM || rl > 0) {
                     const uint32_t u = POLICY == OTH_POLICY_RANDOM ? u_rand : action_draw(rng.seed, id, g);
-#ifdef OTH_ABLATE_SELECT  // timing ablation only: lowest legal square
-                    a = __builtin_ctzll(s.legal.w[0] | (1ull << 63)) + (int)(u & 0);
-#else
                     a = random_action<N>(s, u);
-#endif
                     if (rl > 0) s.meta -= 1u << M_RAND_SHIFT;
                 } else {
-                    a = policy_action<N, POLICY>(s, eng);
+                    a = policy_action<N, POLICY>(s, eng, rng.depth);
                 }
                 step_lane<N, Eng, (bool)OTH_PICKED>(s, a, flags, r, d, win, eng);  // a: a pick from s.legal
                 if (d) {
@@ -1131,7 +1111,6 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
                     }
                 }
             }
-#ifndef OTH_ABLATE_NOSTORE
             if (lead) {
                 if constexpr (REC) {  // running pointers: one 64-bit add each per ply
                     *act_p = a;
@@ -1146,9 +1125,7 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
                     if (dones) dones[o] = (uint8_t)d;
                 }
             }
-#endif
         };
-#if OTH_DRAW_UNROLL && !defined(OTH_ABLATE_RNG)
         if constexpr (POLICY == OTH_POLICY_RANDOM) {
             // Philox block g/4 gives plies 4k..4k+3 their words x, y, z, w: four
             // plies unrolled per block once g is 4-aligned (g is uniform, so
@@ -1168,31 +1145,8 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
                     ++p;
                 }
             }
-        } else
-#endif
-        {
-            U4 draws{0, 0, 0, 0};
-            for (int p = 0; p < plies; ++p) {
-                const uint64_t g = ply0 + (uint64_t)p;
-                // random policy: one Philox block per 4 plies (g uniform: no divergence)
-#ifdef OTH_ABLATE_RNG  // timing ablation only: a multiplicative hash instead of Philox
-                if (POLICY == OTH_POLICY_RANDOM && (p == 0 || (g & 3) == 0)) {
-                    const uint32_t h = (id ^ (uint32_t)g) * 0x9E3779B9u;
-                    draws = U4{h, h * 3u, h * 5u, h * 7u};
-                }
-#else
-                if (POLICY == OTH_POLICY_RANDOM && (p == 0 || (g & 3) == 0)) {
-                    draws = philox4(rng.seed, id, g >> 2, RNG_ACTION);
-#if OTH_DRAW_ROTATE
-                    // draws.x is always this ply's word: rotate to word g % 4 at the launch's first ply
-                    if (p == 0)
-                        for (uint32_t j = 0; j < (uint32_t)(g & 3); ++j) draws = U4{draws.y, draws.z, draws.w, draws.x};
-#endif
-                }
-#endif
-                ply(p, OTH_DRAW_ROTATE ? draws.x : pick4(draws, (uint32_t)(g & 3)));
-                if (POLICY == OTH_POLICY_RANDOM && OTH_DRAW_ROTATE) draws = U4{draws.y, draws.z, draws.w, draws.x};
-            }
+        } else {  // scripted policies draw only on random-opening plies (action_draw inside ply)
+            for (int p = 0; p < plies; ++p) ply(p, 0u);
         }
         if (lead) store_lane<N>(s, boards, meta, legal, e);
     }
@@ -1295,256 +1249,6 @@ __device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_
     }
 }
 
-// PairFills<N>: the Fills engine on a lane pair (lanes 2k, 2k+1; h = 0, 1),
-// one-word boards.  Lane h scans two of the four axes -- h = 0 the E/W and
-// S/N axes, h = 1 the two diagonals -- on dword pairs with per-lane shift
-// amounts (v_lshlrev_b32 / v_alignbit_b32 take the amount from a register, so
-// both lanes run one instruction stream), keeps the fills of its four ray
-// directions and computes their flips from the ray tables (the directions
-// toward lower squares on the turned board, as Fills with OTH_FLIP_TURN 2);
-// moves and flips are or-ed through the pair's DPP swap.  Twice the lanes per
-// board: two waves share each SIMD at 65,536 boards, where one wave alone
-// issues at half the SIMD's rate.
-template <int N>
-struct PairFills {
-    static_assert(Geo<N>::W == 1, "pair fills are for one-word boards (N <= 8)");
-    static constexpr int STEPS = Pro<N, 0, 1>::STEPS;
-    static_assert(STEPS <= 3, "1 + 1 + 2 + 2 doubling");
-    static constexpr uint64_t BD = Geo<N>::BOARD.w[0], IN = Geo<N>::INNER.w[0];
-    const uint64_t* rays;  // lds + 128 h: ray tables of directions 2h, 2h + 1 (+256: the turned 4 + 2h, 5 + 2h)
-    uint32_t sA, rA, sA2, rA2, sB, rB, sB2, rB2;  // axis shifts s, 32 - s, 2s, 32 - 2s
-    U2 mB;                                        // axis B's propagator mask (the vertical axis: whole board)
-    mutable U2 tu[2], td[2];                      // fills of up directions 2h + j and down directions 4 + 2h + j
-    __device__ __forceinline__ PairFills(int h, const uint64_t* lds) {
-        rays = lds + 128 * h;
-        sA = h ? N + 1 : 1;
-        sB = h ? N - 1 : N;
-        rA = 32 - sA;
-        rB = 32 - sB;
-        sA2 = 2 * sA;
-        rA2 = 32 - sA2;
-        sB2 = 2 * sB;
-        rB2 = 32 - sB2;
-        mB = u2(h ? IN : BD);
-    }
-    __device__ __forceinline__ static U2 shl(U2 x, uint32_t s, uint32_t r) {
-        return U2{x.lo << s, __builtin_amdgcn_alignbit(x.hi, x.lo, r)};
-    }
-    __device__ __forceinline__ static U2 shr(U2 x, uint32_t s) {
-        return U2{__builtin_amdgcn_alignbit(x.hi, x.lo, s), x.hi >> s};
-    }
-    // OneWord::axis with the shift in registers
-    __device__ __forceinline__ static void axis(U2 P, U2 p1, uint32_t s, uint32_t r, uint32_t s2, uint32_t r2,
-                                                U2& L, U2& tplus, U2& tminus) {
-        U2 p2{0u, 0u};
-        if constexpr (STEPS > 1) p2 = p1 & shl(p1, s, r);
-        U2 x = shl(P, s, r) & p1;
-        x = (p1 & shl(x, s, r)) | x;
-        if constexpr (STEPS > 1) x = (p2 & shl(x, s2, r2)) | x;
-        if constexpr (STEPS > 2) x = (p2 & shl(x, s2, r2)) | x;
-        tplus = x;
-        L = L | shl(x, s, r);
-        const U2 p2m = shr(p2, s);
-        x = shr(P, s) & p1;
-        x = (p1 & shr(x, s)) | x;
-        if constexpr (STEPS > 1) x = (p2m & shr(x, s2)) | x;
-        if constexpr (STEPS > 2) x = (p2m & shr(x, s2)) | x;
-        tminus = x;
-        L = L | shr(x, s);
-    }
-    // get_possible_actions (othello.py:313-343) for mover Pw; the lane's fills kept
-    __device__ __forceinline__ uint64_t legal(uint64_t Pw, uint64_t Ow) const {
-        const U2 P = u2(Pw), O = u2(Ow);
-        U2 L{0u, 0u};
-        axis(P, O & u2(IN), sA, rA, sA2, rA2, L, td[0], tu[0]);
-        axis(P, O & mB, sB, rB, sB2, rB2, L, td[1], tu[1]);
-        const uint64_t l = u64(L);
-        return (l | pair_swap(l)) & ~(Pw | Ow) & BD;
-    }
-    // update_board's flips (othello.py:391-410) from square a (Fills::flip's form)
-    __device__ __forceinline__ uint64_t flip(int a) const {
-        const uint64_t* r = rays + a;
-        uint64_t f = 0, g = 0;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const uint64_t ray = r[64 * j], t = u64(tu[j]);
-            f |= and3_64(ray, t, (ray & ~t) - 1ull);
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const uint64_t ray = r[256 + 64 * j], tt = OneWord<N>::turn180(u64(td[j]));
-            g |= and3_64(ray, tt, (ray & ~tt) - 1ull);
-        }
-        f |= OneWord<N>::turn180(g);
-        return f | pair_swap(f);
-    }
-};
-
-// The reset position's moves and the lane's fills, computed once per launch.
-template <int N>
-struct PairStart {
-    uint64_t L;
-    U2 tu[2], td[2];
-};
-
-// play_rand_fast on a lane pair (random policy): both lanes hold the board and
-// take the same pick; the scan and the flips are split (PairFills).
-template <int N, bool OPEN>
-__device__ __forceinline__ void play_rand_pair(uint64_t& M, uint64_t& O, uint64_t& L, uint32_t& meta,
-                                               const PairFills<N>& eng, const PairStart<N>& st, uint32_t u,
-                                               uint32_t flags, const Rng& rng, uint32_t id, uint64_t g, int& a,
-                                               int& r, int& d, uint32_t& cb, uint32_t& cd, uint32_t& cw) {
-    constexpr uint64_t BD = Geo<N>::BOARD.w[0];
-    constexpr int NN = N * N;
-    a = select64(L, scale_index(u, popc64(L)));  // RandomPolicy (simple_policies.py:37-41); L != 0
-    if constexpr (OPEN) meta -= (meta & 0xff00u) ? (1u << M_RAND_SHIFT) : 0u;
-    const uint64_t m = 1ull << a;
-    const uint64_t f = eng.flip(a);  // update_board (othello.py:391-410)
-    const uint64_t Mn = M | f | m, On = O & ~f;
-    const bool full = (Mn | On) == BD;  // :425-426
-    uint64_t Ln = eng.legal(On, Mn);    // the opponent's possible_moves (:436)
-    const bool pass = Ln == 0 && !full;
-    if (pass) Ln = eng.legal(Mn, On);  // :437-440 (pair-uniform: Ln is the pair's or)
-    const bool term = full || Ln == 0;
-    const bool swap = !pass && !full;
-    M = swap ? On : Mn;
-    O = swap ? Mn : On;
-    L = Ln;
-    meta ^= swap ? M_TURN_WHITE : 0u;
-    r = 0;
-    d = term ? 1 : 0;
-    if (term) {
-        const bool tw = (meta & M_TURN_WHITE) != 0;
-        const int pc = popc64(Mn), oc = popc64(On);
-        if (flags & OTH_DISK_REWARD) r = oc == 0 ? NN : pc - oc;
-        else r = pc > oc ? 1 : (pc < oc ? -1 : 0);
-        const bool mover_wins = pc > oc, opp_wins = pc < oc;
-        cb += tw ? opp_wins : mover_wins;
-        cd += !mover_wins && !opp_wins;
-        cw += tw ? mover_wins : opp_wins;
-        M = Start<N>::BLACK.w[0];
-        O = Start<N>::WHITE.w[0];
-        L = st.L;
-        eng.tu[0] = st.tu[0];
-        eng.tu[1] = st.tu[1];
-        eng.td[0] = st.td[0];
-        eng.td[1] = st.td[1];
-        uint32_t rl = 0;
-        if (rng.init_rand > 0)
-            rl = (uint32_t)scale_index(philox_x(rng.seed, id, g, RNG_OPENING_AUTO), rng.init_rand / 2 + 1) * 2u;
-        meta = (rl & 0xffu) << M_RAND_SHIFT;
-    }
-}
-
-// k_play_rand<N> on lane pairs (random policy, auto-reset, every output): the
-// same plies, draws and outputs; both lanes of a pair store the same values.
-template <int N>
-__global__ __launch_bounds__(BLOCK) void k_play_rand2(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
-                                                      uint64_t* __restrict__ legal, int E, uint32_t flags, int plies,
-                                                      int32_t* __restrict__ actions, int32_t* __restrict__ rewards,
-                                                      uint8_t* __restrict__ dones,
-                                                      unsigned long long* __restrict__ wdl, Rng rng, uint64_t ply0) {
-    static_assert(Geo<N>::W == 1, "one-word boards");
-    ply0 += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
-    __shared__ __attribute__((aligned(16))) uint64_t lds_rays[8 * 64];
-    const int gt = blockIdx.x * BLOCK + threadIdx.x;
-    const int e = gt >> 1, h = gt & 1;
-    Lane<N> s;
-    if (e < E) load_lane<N>(s, boards, meta, legal, e);
-    fill_rays<N, true>(lds_rays);
-    uint32_t cb = 0, cd = 0, cw = 0;
-    if (e < E) {  // pair-uniform
-        const uint32_t id = rng.id_base + (uint32_t)e;
-        const PairFills<N> eng(h, lds_rays);
-        PairStart<N> st;
-        st.L = eng.legal(Start<N>::BLACK.w[0], Start<N>::WHITE.w[0]);
-        st.tu[0] = eng.tu[0];
-        st.tu[1] = eng.tu[1];
-        st.td[0] = eng.td[0];
-        st.td[1] = eng.td[1];
-        const bool tw0 = (s.meta & M_TURN_WHITE) != 0;
-        uint64_t M = tw0 ? s.white.w[0] : s.black.w[0];
-        uint64_t O = tw0 ? s.black.w[0] : s.white.w[0];
-        uint64_t L = s.legal.w[0];
-        uint32_t mt = s.meta & (0xff00u | M_TURN_WHITE);
-        (void)eng.legal(M, O);  // the mover's fills
-        const bool slow = __any((s.meta & M_TERMINATED) != 0);
-        int32_t* act_p = actions + e;
-        int32_t* rew_p = rewards + e;
-        uint8_t* done_p = dones + e;
-        auto fast = [&](auto OPENC) __attribute__((always_inline)) {
-            constexpr bool OPEN = decltype(OPENC)::value;
-            auto ply = [&](int p, uint32_t u) __attribute__((always_inline)) {
-                int a, r, d;
-                play_rand_pair<N, OPEN>(M, O, L, mt, eng, st, u, flags, rng, id, ply0 + (uint64_t)p, a, r, d, cb, cd,
-                                        cw);
-                *act_p = a;  // both lanes of the pair: the same value to the same address
-                *rew_p = r;
-                *done_p = (uint8_t)d;
-                act_p += E;
-                rew_p += E;
-                done_p += E;
-            };
-            int p = 0;
-            while (p < plies && ((ply0 + (uint64_t)p) & 3) != 0) {
-                const uint64_t g = ply0 + (uint64_t)p;
-                ply(p, pick4(philox4(rng.seed, id, g >> 2, RNG_ACTION), (uint32_t)(g & 3)));
-                ++p;
-            }
-            if (p + 4 <= plies) {
-                U4 cur = philox4(rng.seed, id, (ply0 + (uint64_t)p) >> 2, RNG_ACTION);
-                while (p + 4 <= plies) {
-                    const U4 nxt = p + 8 <= plies ? philox4(rng.seed, id, ((ply0 + (uint64_t)p) >> 2) + 1, RNG_ACTION)
-                                                  : cur;
-                    ply(p, cur.x);
-                    ply(p + 1, cur.y);
-                    ply(p + 2, cur.z);
-                    ply(p + 3, cur.w);
-                    cur = nxt;
-                    p += 4;
-                }
-            }
-            while (p < plies) {
-                const uint64_t g = ply0 + (uint64_t)p;
-                ply(p, pick4(philox4(rng.seed, id, g >> 2, RNG_ACTION), (uint32_t)(g & 3)));
-                ++p;
-            }
-        };
-        if (!slow) {
-            if (OTH_OPEN_SPLIT && rng.init_rand == 0 && !__any((mt & 0xff00u) != 0)) fast(std::false_type{});
-            else fast(std::true_type{});
-            const bool tw = (mt & M_TURN_WHITE) != 0;
-            s.white.w[0] = tw ? M : O;
-            s.black.w[0] = tw ? O : M;
-            s.legal.w[0] = L;
-            s.meta = mt;
-        } else {  // a board loaded terminated in the wave (k_play's semantics): both lanes step alone
-            const Solo<N> solo(0, nullptr);
-            for (int p = 0; p < plies; ++p) {
-                const uint64_t g = ply0 + (uint64_t)p;
-                int a = -1, r = 0, d = 1, win = NO_DISK;
-                if (!(s.meta & M_TERMINATED)) {
-                    a = random_action<N>(s, action_draw(rng.seed, id, g));
-                    if ((s.meta >> M_RAND_SHIFT) > 0) s.meta -= 1u << M_RAND_SHIFT;
-                    step_lane<N>(s, a, flags, r, d, win, solo);
-                    if (d) {
-                        cb += win == BLACK_DISK;
-                        cd += win == NO_DISK;
-                        cw += win == WHITE_DISK;
-                        reset_lane<N>(s, rng.seed, id, g, RNG_OPENING_AUTO, rng.init_rand);
-                    }
-                }
-                act_p[(size_t)p * E] = a;
-                rew_p[(size_t)p * E] = r;
-                done_p[(size_t)p * E] = (uint8_t)d;
-            }
-        }
-        if (h == 0) store_lane<N>(s, boards, meta, legal, e);
-    }
-    if (h) cb = cd = cw = 0;  // one count per board
-    tally(wdl, cb, cd, cw);
-}
-
 template <int N, int POLICY = OTH_POLICY_RANDOM>
 __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
                                                      uint64_t* __restrict__ legal, int E, uint32_t flags, int plies,
@@ -1554,22 +1258,12 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
     static_assert(Geo<N>::W == 1, "one-word boards");
     ply0 += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
     __shared__ __attribute__((aligned(16))) uint64_t lds_rays[Fills<N>::RAY_WORDS];
-#if OTH_RAYS_REP
-    __shared__ __attribute__((aligned(16))) ulonglong2 lds_rep[REP_ENTRIES];
-    fill_rays<N, turned_rays<Fills<N>>::value, false>(lds_rays);  // the generic loop's table (boards loaded terminated)
-    fill_rays_rep<N>(lds_rep);
-#else
     fill_rays<N, turned_rays<Fills<N>>::value>(lds_rays);
-#endif
     const int e = blockIdx.x * BLOCK + threadIdx.x;
     uint32_t cb = 0, cd = 0, cw = 0;
     if (e < E) {
         const uint32_t id = rng.id_base + (uint32_t)e;
-#if OTH_RAYS_REP
-        const FillsRep<N> eng(lds_rays, lds_rep);
-#else
         const Fills<N> eng(0, lds_rays);
-#endif
         Lane<N> s;
         load_lane<N>(s, boards, meta, legal, e);
         const bool tw0 = (s.meta & M_TURN_WHITE) != 0;
@@ -1578,9 +1272,13 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
         uint64_t L = s.legal.w[0];
         uint32_t mt = s.meta & (0xff00u | M_TURN_WHITE);
         eng.prime(s);
-        // a board loaded terminated stays so (k_play's semantics); such a wave
-        // is rare (set_state) and takes the generic loop below
-        const bool slow = __any((s.meta & M_TERMINATED) != 0);
+        // a board loaded terminated stays so (k_play's semantics), and a live board
+        // loaded with no possible move takes the invalid path (othello.py:417-427,
+        // possible_moves == [] before a reset, :242); such a wave is rare
+        // (set_state) and takes the generic loop below.  Inside the fast loop no
+        // live board has L == 0: a pass re-scans, a double pass terminates and
+        // auto-resets.
+        const bool slow = __any((s.meta & M_TERMINATED) != 0 || L == 0);
         int32_t* act_p = actions + e;
         int32_t* rew_p = rewards + e;
         uint8_t* done_p = dones + e;
@@ -1589,7 +1287,7 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
         auto ply = [&](int p, uint32_t u, const auto& fill) __attribute__((always_inline)) {
             int a, r, d;
             play_rand_fast<N, POLICY, OPEN>(M, O, L, mt, eng, u, flags, rng, id, ply0 + (uint64_t)p, a, r, d, cb, cd,
-                                            cw, fill);  // (Eng deduced: FillsRep with OTH_RAYS_REP)
+                                            cw, fill);
             *act_p = a;
             *rew_p = r;
             *done_p = (uint8_t)d;
@@ -1773,7 +1471,7 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand_w(uint64_t* __restrict__ bo
         }
         uint32_t mt = s.meta & (0xff00u | M_TURN_WHITE);
         eng.prime(s);
-        const bool slow = __any((s.meta & M_TERMINATED) != 0);
+        const bool slow = __any((s.meta & M_TERMINATED) != 0 || !any(L));  // as k_play_rand
         int32_t* act_p = actions + e;
         int32_t* rew_p = rewards + e;
         uint8_t* done_p = dones + e;
@@ -1838,269 +1536,6 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand_w(uint64_t* __restrict__ bo
 }
 
 
-// oth_sample_step: the learners' per-ply loop in one launch -- the masked
-// categorical over each board's possible_moves (Policy.act, model.py:60-99;
-// PPO.get_action, ppo.py:228-262) immediately followed by OthelloBaseEnv.step
-// (othello.py:412-462) with the sampled action.  The sampling runs the very
-// code of k_masked (masked.hpp) with its G lanes per board: lane group g
-// samples its G boards g*G .. g*G+G-1 one after the other and lane l keeps
-// board g*G+l's pick, which is the board it then steps (one lane per board,
-// as k_step).  So the results are bit-identical to oth_sample_actions +
-// oth_step, with one launch and no actions round trip through memory.
-// ONE (boards of up to two words): each lane samples its own board with
-// oth_ms::sample_lane, the group's arithmetic restated for one lane.
-template <int N, int G, bool VEC, bool FULL, bool ONE>
-__global__ __launch_bounds__(BLOCK) void k_sample_step(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
-                                                       uint64_t* __restrict__ legal, int E, uint32_t flags,
-                                                       const float* __restrict__ logits, long long ld,
-                                                       const float* __restrict__ uniforms, uint64_t counter, int mode,
-                                                       int32_t* __restrict__ actions, float* __restrict__ log_probs,
-                                                       float* __restrict__ entropy, int32_t* __restrict__ rewards,
-                                                       uint8_t* __restrict__ dones,
-                                                       unsigned long long* __restrict__ wdl, Rng rng, uint64_t ply) {
-    constexpr int NN = N * N;
-    constexpr int CH = Geo<N>::W;
-    ply += rng.ply_off[0];      // graph-region offsets (oth_graph_end); 0 eagerly
-    counter += rng.ply_off[1];  // the sample counter's, as k_masked
-    const long long t = (long long)blockIdx.x * BLOCK + threadIdx.x;
-    const int l = (int)(t % G);
-    const long long g0 = (t / G) * G;
-    const bool mine_live = t < E;
-    // the board this lane steps: its loads are issued before the sampling, so
-    // they are in flight while the group samples
-    Lane<N> s;
-    if (mine_live) load_lane<N>(s, boards, meta, legal, (int)t);
-    oth_ms::Pick mine{0, 0.f, 0.f};
-    if constexpr (ONE) {  // one lane per board: the group's arithmetic restated per lane (oth_ms::sample_lane)
-        const oth_ms::f32x4* row = nullptr;
-        if constexpr (VEC && OTH_SS_STAGE) {  // the wave's 64 rows through LDS: coalesced loads
-            constexpr int QN = NN / 4;
-            __shared__ oth_ms::f32x4 stage[(BLOCK / 64) * 64 * (QN + 1)];
-            const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-            oth_ms::f32x4* ws = stage + wv * 64 * (QN + 1);
-            oth_ms::stage_rows<QN>(ws, t - lane, E, logits, ld, lane);
-            __syncthreads();
-            row = ws + lane * (QN + 1);
-        }
-#if OTH_SS_ABL  // timing ablations (tools/ab_sample_step.py): 1 no sampling, 2 the logits loads only
-        if (mine_live) {
-            const uint64_t lw = s.legal.w[0];
-            mine.a = lw ? __builtin_ctzll(lw) : 0;
-            if (OTH_SS_ABL == 2) {
-                const float* rw = logits + (size_t)t * (size_t)ld;
-                float acc = 0.f;
-#pragma unroll
-                for (int q = 0; q < NN; q += 4) {
-                    const oth_ms::f32x4 v = *reinterpret_cast<const oth_ms::f32x4*>(rw + q);
-                    acc += (v.x + v.y) + (v.z + v.w);
-                }
-                if (acc == 12345.f) mine.a = 1;
-            }
-        }
-        if (false)
-#else
-        if (mine_live)
-#endif
-            mine = oth_ms::sample_lane<CH, G, VEC, FULL>((int)t, NN, logits, ld, legal, uniforms, rng.seed,
-                                                         rng.id_base, counter, mode, 0, log_probs != nullptr,
-                                                         entropy != nullptr, row);
-    } else {
-    constexpr int BATCH = G < 4 ? G : 4;  // boards whose logits loads are issued together
-#pragma unroll 1
-    for (int k0 = 0; k0 < G; k0 += BATCH) {
-        oth_ms::Slot<CH, G> b[BATCH];
-#pragma unroll
-        for (int k = 0; k < BATCH; ++k) {
-            const long long eb = g0 + k0 + k;
-            b[k].live = eb < E;
-            b[k].e = b[k].live ? (int)eb : E - 1;  // dead boards still take part in the group's DPP steps
-            oth_ms::load_slot<CH, G, VEC>(b[k], l, NN, logits, ld, legal);
-        }
-#pragma unroll
-        for (int k = 0; k < BATCH; ++k) {
-            const oth_ms::Pick pk = oth_ms::finish_slot<CH, G, FULL>(b[k], l, NN, logits, ld, uniforms, rng.seed,
-                                                                     rng.id_base, counter, mode, 0,
-                                                                     log_probs != nullptr, entropy != nullptr);
-            if (k0 + k == l) mine = pk;
-        }
-    }
-    }
-    uint32_t cb = 0, cd = 0, cw = 0;
-    if (mine_live) {
-        const int e = (int)t;
-        actions[e] = mine.a;
-        if (log_probs) log_probs[e] = mine.lp;
-        if (entropy) entropy[e] = mine.ent;
-        const bool was_term = (s.meta & M_TERMINATED) != 0;
-        int r, d, win;
-        step_lane<N>(s, mine.a, flags, r, d, win, Solo<N>(0, nullptr));
-        if (d && !was_term) {
-            cb = win == BLACK_DISK;
-            cd = win == NO_DISK;
-            cw = win == WHITE_DISK;
-            if (flags & OTH_AUTO_RESET)
-                reset_lane<N>(s, rng.seed, rng.id_base + (uint32_t)e, ply, RNG_OPENING_AUTO, rng.init_rand);
-        }
-        store_lane<N>(s, boards, meta, legal, e);
-        if (rewards) rewards[e] = r;
-        if (dones) dones[e] = (uint8_t)d;
-    }
-    tally(wdl, cb, cd, cw);
-}
-
-// k_sample_step on lane pairs (one-word boards): the pair samples its board
-// with oth_ms::sample_pair (bit-identical to the one-lane form) and steps it
-// with the Duo engine (half the axes and rays per lane, or-ed through DPP).
-// Twice the waves of k_sample_step for the same boards, so two waves share
-// each SIMD at 65,536 boards: the loads of one hide behind the other's VALU
-// work, and the pair halves the per-lane sampling and scanning.
-template <int N, bool VEC, bool FULL>
-__global__ __launch_bounds__(BLOCK) void k_sample_step2(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
-                                                        uint64_t* __restrict__ legal, int E, uint32_t flags,
-                                                        const float* __restrict__ logits, long long ld,
-                                                        const float* __restrict__ uniforms, uint64_t counter,
-                                                        int mode, int32_t* __restrict__ actions,
-                                                        float* __restrict__ log_probs, float* __restrict__ entropy,
-                                                        int32_t* __restrict__ rewards, uint8_t* __restrict__ dones,
-                                                        unsigned long long* __restrict__ wdl, Rng rng, uint64_t ply) {
-    constexpr int W = Geo<N>::W;
-    static_assert(W <= 2 && OTH_MS_G == 4, "lane pairs restate k_masked's four lanes of boards of <= 2 words");
-    constexpr int NN = N * N;
-    ply += rng.ply_off[0];      // graph-region offsets (oth_graph_end); 0 eagerly
-    counter += rng.ply_off[1];  // the sample counter's, as k_masked
-    // the step's engine: Duo (one-word boards: half the axes and rays per lane) or, OTH_SS2_SOLO and
-    // on two-word boards, each lane the whole step (the pair's lanes agree: same inputs) without ray
-    // tables, LDS or a barrier
-    constexpr bool SOLO = OTH_SS2_SOLO != 0 || W == 2;
-    using Eng = typename std::conditional<SOLO, Solo<N>, Duo<N>>::type;
-    __shared__ __attribute__((aligned(16))) uint64_t lds_rays[SOLO ? 1 : 8 * 64];
-    const long long gt = (long long)blockIdx.x * BLOCK + threadIdx.x;
-    const int e = (int)(gt >> 1), h = (int)(gt & 1);
-    const Eng eng(h, lds_rays);
-    uint32_t cb = 0, cd = 0, cw = 0;
-    Lane<N> s;  // the board's loads are issued first, in flight with the logits loads
-    if (e < E) load_lane<N>(s, boards, meta, legal, e);
-    auto board = [&](auto STAGEDC, const oth_ms::f32x4* staged) __attribute__((always_inline)) {
-        if (e >= E) return;  // pair-uniform: both lanes of a pair share e
-#if OTH_SS_ABL  // timing ablations (tools/ab_sample_step.py --no-check): 1 no sampling, 2 loads only, 3 no step
-        oth_ms::Pick pk{s.legal.w[0] ? (int)__builtin_ctzll(s.legal.w[0]) : 0, 0.f, 0.f};
-        if (OTH_SS_ABL == 2) {
-            const float* rw = logits + (size_t)e * (size_t)ld + 32 * h;
-            float acc = 0.f;
-#pragma unroll
-            for (int q = 0; q < 32; q += 4) {
-                const oth_ms::f32x4 v = *reinterpret_cast<const oth_ms::f32x4*>(rw + q);
-                acc += (v.x + v.y) + (v.z + v.w);
-            }
-            if (acc == 12345.f) pk.a = 1;
-        }
-        if (OTH_SS_ABL == 3)
-            pk = oth_ms::sample_pair<W, VEC, FULL, decltype(STAGEDC)::value>(
-                e, h, NN, logits, ld, s.legal.w, uniforms, rng.seed, rng.id_base, counter, mode,
-                log_probs != nullptr, entropy != nullptr, staged);
-#else
-        const oth_ms::Pick pk = oth_ms::sample_pair<W, VEC, FULL, decltype(STAGEDC)::value>(
-            e, h, NN, logits, ld, s.legal.w, uniforms, rng.seed, rng.id_base, counter, mode, log_probs != nullptr,
-            entropy != nullptr, staged);
-#endif
-        const bool was_term = (s.meta & M_TERMINATED) != 0;
-        int r = 0, d = 0, win = NO_DISK;
-        if (OTH_SS_ABL != 3) step_lane<N>(s, pk.a, flags, r, d, win, eng);
-        if (d && !was_term) {
-            if (h == 0) {
-                cb = win == BLACK_DISK;
-                cd = win == NO_DISK;
-                cw = win == WHITE_DISK;
-            }
-            if (flags & OTH_AUTO_RESET)
-                reset_lane<N>(s, rng.seed, rng.id_base + (uint32_t)e, ply, RNG_OPENING_AUTO, rng.init_rand);
-        }
-        if (h == 0) {
-            actions[e] = pk.a;
-            if (log_probs) log_probs[e] = pk.lp;
-            if (entropy) entropy[e] = pk.ent;
-            store_lane<N>(s, boards, meta, legal, e);
-            if (rewards) rewards[e] = r;
-            if (dones) dones[e] = (uint8_t)d;
-        }
-    };
-    // the ray tables are built after the loads are issued (their latency hides the build)
-    if constexpr (VEC && N == 8 && OTH_SS2_STAGE) {  // the wave's 32 rows through LDS: coalesced loads
-        __shared__ oth_ms::f32x4 stage[(BLOCK / 64) * 32 * oth_ms::PAIR_ROW];
-        const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-        oth_ms::f32x4 v[8];
-        oth_ms::load_pair_rows(v, (gt - lane) >> 1, E, logits, ld, lane);
-        if constexpr (!SOLO) fill_rays<N, false, false>(lds_rays);  // while the rows are in flight
-        const oth_ms::f32x4* rows = oth_ms::store_pair_rows(stage + wv * 32 * oth_ms::PAIR_ROW, v, lane);
-        __syncthreads();  // the ray tables (the rows need only the wave's own order)
-        board(std::true_type{}, rows);
-    } else {
-        if constexpr (!SOLO) fill_rays<N, false>(lds_rays);
-        board(std::false_type{}, nullptr);
-    }
-    tally(wdl, cb, cd, cw);
-}
-
-// k_sample_step on lane quads (one-word boards): the quad IS k_masked's group
-// of G = 4 lanes for the board (load_slot / finish_slot, the same code, so the
-// pick is k_masked's), then steps it with the Quartet engine.  Four times the
-// waves of the one-lane form: each lane's instruction stream is a quarter of
-// the sampling and of the scans, and four waves share each SIMD.
-template <int N, bool VEC, bool FULL>
-__global__ __launch_bounds__(BLOCK) void k_sample_step4(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
-                                                        uint64_t* __restrict__ legal, int E, uint32_t flags,
-                                                        const float* __restrict__ logits, long long ld,
-                                                        const float* __restrict__ uniforms, uint64_t counter,
-                                                        int mode, int32_t* __restrict__ actions,
-                                                        float* __restrict__ log_probs, float* __restrict__ entropy,
-                                                        int32_t* __restrict__ rewards, uint8_t* __restrict__ dones,
-                                                        unsigned long long* __restrict__ wdl, Rng rng, uint64_t ply) {
-    static_assert(Geo<N>::W == 1 && OTH_MS_G == 4, "lane quads are k_masked's four lanes of one-word boards");
-    constexpr int NN = N * N;
-    ply += rng.ply_off[0];      // graph-region offsets (oth_graph_end); 0 eagerly
-    counter += rng.ply_off[1];  // the sample counter's, as k_masked
-    __shared__ __attribute__((aligned(16))) uint64_t lds_rays[Quartet<N>::RAY_WORDS];
-    const long long gt = (long long)blockIdx.x * BLOCK + threadIdx.x;
-    const int e = (int)(gt >> 2), q = (int)(gt & 3);
-    const Quartet<N> eng(q, lds_rays);
-    uint32_t cb = 0, cd = 0, cw = 0;
-    Lane<N> s;  // the board's and the logits' loads are issued before the ray tables are built
-    oth_ms::Slot<1, 4> b;
-    b.e = e;
-    b.live = e < E;
-    if (e < E) {
-        load_lane<N>(s, boards, meta, legal, e);
-        oth_ms::load_slot<1, 4, VEC>(b, q, NN, logits, ld, legal);
-    }
-    fill_rays<N, false>(lds_rays);
-    if (e < E) {  // quad-uniform: the four lanes of a quad share e
-        const oth_ms::Pick pk = oth_ms::finish_slot<1, 4, FULL>(b, q, NN, logits, ld, uniforms, rng.seed, rng.id_base,
-                                                                counter, mode, 0, log_probs != nullptr,
-                                                                entropy != nullptr);
-        const bool was_term = (s.meta & M_TERMINATED) != 0;
-        int r, d, win;
-        step_lane<N>(s, pk.a, flags, r, d, win, eng);
-        if (d && !was_term) {
-            if (q == 0) {
-                cb = win == BLACK_DISK;
-                cd = win == NO_DISK;
-                cw = win == WHITE_DISK;
-            }
-            if (flags & OTH_AUTO_RESET)
-                reset_lane<N>(s, rng.seed, rng.id_base + (uint32_t)e, ply, RNG_OPENING_AUTO, rng.init_rand);
-        }
-        if (q == 0) {
-            actions[e] = pk.a;
-            if (log_probs) log_probs[e] = pk.lp;
-            if (entropy) entropy[e] = pk.ent;
-            store_lane<N>(s, boards, meta, legal, e);
-            if (rewards) rewards[e] = r;
-            if (dones) dones[e] = (uint8_t)d;
-        }
-    }
-    tally(wdl, cb, cd, cw);
-}
-
 // ---------------------------------------------------------------------------
 // OthelloEnv semantics on the device (othello.py:151-200): the protagonist
 // steps with the caller's action, then the embedded opponent (random or greedy,
@@ -2125,7 +1560,7 @@ __device__ __forceinline__ void opponent_reply(Lane<N>& s, bool prot_white, bool
         if (POLICY == OTH_POLICY_RANDOM || (openings && rl > 0)) {
             a = random_action<N>(s, action_draw(rng.seed, id, g));
         } else {
-            a = policy_action<N, POLICY>(s, eng);
+            a = policy_action<N, POLICY>(s, eng, rng.depth);
         }
         if (openings && rl > 0) s.meta -= 1u << M_RAND_SHIFT;
         step_lane<N>(s, a, flags, r, d, win, eng);
@@ -2242,12 +1677,12 @@ template <int N, int POLICY>
 __global__ __launch_bounds__(BLOCK) void k_policy_actions(const uint64_t* __restrict__ boards,
                                                           const uint16_t* __restrict__ meta,
                                                           const uint64_t* __restrict__ legal, int E,
-                                                          int32_t* __restrict__ out) {
+                                                          int32_t* __restrict__ out, int depth) {
     const int e = blockIdx.x * BLOCK + threadIdx.x;
     if (e >= E) return;
     Lane<N> s;
     load_lane<N>(s, boards, meta, legal, e);
-    out[e] = policy_action<N, POLICY>(s, Solo<N>(0, nullptr));
+    out[e] = policy_action<N, POLICY>(s, Solo<N>(0, nullptr), depth);
 }
 
 template <int N>

@@ -4,6 +4,8 @@
 
 #include "device.hpp"
 #include "launch.hpp"
+#include "ply.hpp"
+#include "sample_step.hpp"
 
 #ifndef OTH_N
 #error "compile with -DOTH_N=<board size>"
@@ -17,7 +19,11 @@ namespace {
 
 int grid_for(long long work) { return (int)((work + BLOCK - 1) / BLOCK); }
 
-Rng rng_of(const oth_env* env) { return Rng{env->seed, env->id_base, env->init_rand, env->cur_off}; }
+// policy: an OTH_POLICY_* id; MaxiMin of depth >= 4 reads its depth from the Rng
+Rng rng_of(const oth_env* env, int policy = OTH_POLICY_RANDOM) {
+    const int depth = policy >= OTH_POLICY_MAXIMIN1 ? policy - OTH_POLICY_MAXIMIN1 + 1 : 0;
+    return Rng{env->seed, env->id_base, env->init_rand, env->cur_off, depth};
+}
 
 // Compile-time policy for a runtime id (OTH_POLICY_*); MAXIMIN1 is GREEDY
 // (same move: simple_policies.py:111-155 at depth 1 is GreedyPolicy's argmax).
@@ -29,7 +35,10 @@ int with_policy(int policy, Fn&& fn) {
         case OTH_POLICY_MAXIMIN1: return fn(std::integral_constant<int, OTH_POLICY_GREEDY>{});
         case OTH_POLICY_MAXIMIN2: return fn(std::integral_constant<int, OTH_POLICY_MAXIMIN2>{});
         case OTH_POLICY_MAXIMIN3: return fn(std::integral_constant<int, OTH_POLICY_MAXIMIN3>{});
-        default: return fail(OTH_EINVAL, "unknown policy");
+        default:
+            if (policy > OTH_POLICY_MAXIMIN3 && policy <= OTH_POLICY_LAST)  // depth 4 .. OTH_MAXIMIN_MAX_DEPTH
+                return fn(std::integral_constant<int, OTH_POLICY_MAXIMIN_DEEP>{});
+            return fail(OTH_EINVAL, "unknown policy");
     }
 }
 
@@ -42,9 +51,25 @@ int launch_reset(oth_env* env, const uint8_t* mask, hipStream_t st) {
     return after_launch("oth_reset");
 }
 
+// oth_create for one-word boards: the single-ply kernels' ray table
+template <int N>
+int launch_fill_rays(oth_env* env, hipStream_t st) {
+    if constexpr (Geo<N>::W == 1) {
+        hipLaunchKernelGGL(k_fill_rays<N>, dim3(1), dim3(BLOCK), 0, st, env->rays);
+        return after_launch("oth_create: ray table");
+    }
+    return OTH_OK;
+}
+
 template <int N>
 int launch_step(oth_env* env, const int32_t* actions, int32_t* rewards, uint8_t* dones, uint64_t ply,
                 hipStream_t st) {
+    if constexpr (Geo<N>::W == 1) {  // the single-ply kernel (ply.hpp)
+        hipLaunchKernelGGL((k_ply_step<N>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards, env->meta,
+                           env->legal, env->E, env->flags, actions, rewards, dones, env->wdl, env->rays, rng_of(env),
+                           ply);
+        return after_launch("oth_step");
+    }
     hipLaunchKernelGGL(k_step<N>, dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards, env->meta, env->legal,
                        env->E, env->flags, actions, rewards, dones, env->wdl, rng_of(env), ply);
     return after_launch("oth_step");
@@ -53,17 +78,19 @@ int launch_step(oth_env* env, const int32_t* actions, int32_t* rewards, uint8_t*
 // k_play with the REC specialisation where all per-ply outputs are stored
 // (random / greedy only, to bound the number of maximin instantiations).
 template <int N, int POL, typename Eng>
-void launch_k_play(int lanes_per_board, oth_env* env, int n_plies, int32_t* actions, int32_t* rewards,
+void launch_k_play(int lanes_per_board, oth_env* env, int policy, int n_plies, int32_t* actions, int32_t* rewards,
                    uint8_t* dones, uint64_t ply0, hipStream_t st) {
     const dim3 grid(grid_for((long long)lanes_per_board * env->E)), block(BLOCK);
+    if constexpr (POL == OTH_POLICY_RANDOM && Geo<N>::W == 1) {
+        if (n_plies == 1) {  // one ply per launch: the single-ply kernel (ply.hpp), any flags
+            hipLaunchKernelGGL((k_ply_rand<N>), dim3(grid_for(env->E)), block, 0, st, env->boards, env->meta,
+                               env->legal, env->E, env->flags, actions, rewards, dones, env->wdl, env->rays,
+                               rng_of(env), ply0);
+            return;
+        }
+    }
     if constexpr (OTH_FAST_RANDOM && POL == OTH_POLICY_RANDOM && std::is_same<Eng, Fills<N>>::value) {
         if (actions && rewards && dones && (env->flags & OTH_AUTO_RESET)) {
-            if (OTH_PLAY_PAIR && grid_for(2LL * env->E) <= env->nslots) {  // lane pairs (k_play_rand2)
-                hipLaunchKernelGGL((k_play_rand2<N>), dim3(grid_for(2LL * env->E)), block, 0, st, env->boards,
-                                   env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards, dones,
-                                   env->wdl, rng_of(env), ply0);
-                return;
-            }
             launch_play_rand<N, OTH_POLICY_RANDOM>(env, n_plies, actions, rewards, dones, ply0, st);  // play_rand_n.hip
             return;
         }
@@ -77,19 +104,19 @@ void launch_k_play(int lanes_per_board, oth_env* env, int n_plies, int32_t* acti
     if constexpr (OTH_FAST_RANDOM_W && POL == OTH_POLICY_RANDOM && std::is_same<Eng, FillsW<N>>::value) {
         if (actions && rewards && dones && (env->flags & OTH_AUTO_RESET)) {
             hipLaunchKernelGGL((k_play_rand_w<N>), grid, block, 0, st, env->boards, env->meta, env->legal, env->E,
-                               env->flags, n_plies, actions, rewards, dones, env->wdl, rng_of(env), ply0);
+                               env->flags, n_plies, actions, rewards, dones, env->wdl, rng_of(env, policy), ply0);
             return;
         }
     }
     if constexpr (OTH_REC_TEMPLATE && (POL == OTH_POLICY_RANDOM || POL == OTH_POLICY_GREEDY)) {
         if (actions && rewards && dones) {
             hipLaunchKernelGGL((k_play<N, POL, Eng, true>), grid, block, 0, st, env->boards, env->meta, env->legal,
-                               env->E, env->flags, n_plies, actions, rewards, dones, env->wdl, rng_of(env), ply0);
+                               env->E, env->flags, n_plies, actions, rewards, dones, env->wdl, rng_of(env, policy), ply0);
             return;
         }
     }
     hipLaunchKernelGGL((k_play<N, POL, Eng, false>), grid, block, 0, st, env->boards, env->meta, env->legal, env->E,
-                       env->flags, n_plies, actions, rewards, dones, env->wdl, rng_of(env), ply0);
+                       env->flags, n_plies, actions, rewards, dones, env->wdl, rng_of(env, policy), ply0);
 }
 
 template <int N>
@@ -97,21 +124,19 @@ int launch_play(oth_env* env, int policy, int n_plies, int32_t* actions, int32_t
                 uint64_t ply0, hipStream_t st) {
     return with_policy(policy, [&](auto PC) {
         constexpr int POL = decltype(PC)::value;
-        if constexpr (Geo<N>::W == 1 && OTH_DUO && POL == OTH_POLICY_RANDOM) {
-            launch_k_play<N, POL, Duo<N>>(2, env, n_plies, actions, rewards, dones, ply0, st);
-        } else if constexpr (Geo<N>::W == 1 && OTH_FILLS &&
+        if constexpr (Geo<N>::W == 1 && OTH_FILLS &&
                              (POL == OTH_POLICY_RANDOM || (OTH_FILLS_GREEDY && POL == OTH_POLICY_GREEDY))) {
-            launch_k_play<N, POL, Fills<N>>(1, env, n_plies, actions, rewards, dones, ply0, st);
+            launch_k_play<N, POL, Fills<N>>(1, env, policy, n_plies, actions, rewards, dones, ply0, st);
         } else if constexpr (Geo<N>::W > 1 && OTH_FILLS_W && N <= OTH_FILLS_W_MAXN &&
                              (POL == OTH_POLICY_RANDOM || POL == OTH_POLICY_GREEDY)) {
-            launch_k_play<N, POL, FillsW<N>>(1, env, n_plies, actions, rewards, dones, ply0, st);
+            launch_k_play<N, POL, FillsW<N>>(1, env, policy, n_plies, actions, rewards, dones, ply0, st);
         } else if constexpr (Geo<N>::W == 1 && OTH_RAYS && POL == OTH_POLICY_RANDOM) {
             // random play with OTH_FILLS=0: ray-table flips with the capping test
             // (greedy keeps Kogge-Stone flips there: the ray tables' exposed LDS
             // latency measured -10 % for greedy without the fills)
-            launch_k_play<N, POL, Rays<N>>(1, env, n_plies, actions, rewards, dones, ply0, st);
+            launch_k_play<N, POL, Rays<N>>(1, env, policy, n_plies, actions, rewards, dones, ply0, st);
         } else {
-            launch_k_play<N, POL, Solo<N>>(1, env, n_plies, actions, rewards, dones, ply0, st);
+            launch_k_play<N, POL, Solo<N>>(1, env, policy, n_plies, actions, rewards, dones, ply0, st);
         }
         return after_launch("oth_step_policy");
     });
@@ -189,7 +214,7 @@ int launch_reset_vs(oth_env* env, int policy, const int8_t* prot, const uint8_t*
     return with_policy(policy, [&](auto PC) {
         constexpr int POL = decltype(PC)::value;
         hipLaunchKernelGGL((k_reset_vs<N, POL>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards, env->meta,
-                           env->legal, env->E, env->flags, prot, mask, rng_of(env), call);
+                           env->legal, env->E, env->flags, prot, mask, rng_of(env, policy), call);
         return after_launch("oth_reset_vs");
     });
 }
@@ -201,7 +226,7 @@ int launch_step_vs(oth_env* env, int policy, const int32_t* actions, const int8_
         constexpr int POL = decltype(PC)::value;
         hipLaunchKernelGGL((k_step_vs<N, POL>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards, env->meta,
                            env->legal, env->E, env->flags, actions, prot, rewards, dones, plies, env->wdl,
-                           env->wdl_vs, rng_of(env), call);
+                           env->wdl_vs, rng_of(env, policy), call);
         return after_launch("oth_step_vs");
     });
 }
@@ -212,7 +237,7 @@ int launch_policy_actions(oth_env* env, int policy, int32_t* out, hipStream_t st
         constexpr int POL = decltype(PC)::value;
         if constexpr (POL != OTH_POLICY_RANDOM)
             hipLaunchKernelGGL((k_policy_actions<N, POL>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards,
-                               env->meta, env->legal, env->E, out);
+                               env->meta, env->legal, env->E, out, rng_of(env, policy).depth);
         return after_launch("oth_policy_actions");
     });
 }
@@ -327,5 +352,6 @@ template int launch_legal_moves<OTH_N>(int, const uint64_t*, const uint64_t*, ui
 template int launch_observe<OTH_N>(oth_env*, int, int, void*, hipStream_t);
 template int launch_set_turn<OTH_N>(oth_env*, int, const uint8_t*, hipStream_t);
 template int launch_count<OTH_N>(oth_env*, int32_t*, hipStream_t);
+template int launch_fill_rays<OTH_N>(oth_env*, hipStream_t);
 
 }  // namespace oth_host

@@ -31,8 +31,9 @@ struct oth_env {
     uint64_t* ctr_slots;
     const uint64_t* cur_off;  // the slot launches read now (slot 0 outside a region)
     int32_t graph_slot;       // open region (0: none)
-    int32_t next_slot;        // next free slot
+    uint64_t slots_used;      // bit k: slot k belongs to a captured graph (bit 0, eager, always set)
     uint64_t ply_saved;       // eager ply counter while a region is open
+    uint64_t* rays;           // one-word boards: the 8 x 64 ray table of the single-ply kernel (ply.hpp)
 };
 
 namespace oth_host {
@@ -71,6 +72,7 @@ int launch_legal_moves(int n, const uint64_t* mover, const uint64_t* opp, uint64
 template <int N> int launch_observe(oth_env* env, int layout, int dtype, void* out, hipStream_t st);
 template <int N> int launch_set_turn(oth_env* env, int turn, const uint8_t* mask, hipStream_t st);
 template <int N> int launch_count(oth_env* env, int32_t* out, hipStream_t st);
+template <int N> int launch_fill_rays(oth_env* env, hipStream_t st);
 // k_play_rand for one-word boards (play_rand_n.hip, N = 4..8, its own scheduler flags)
 template <int N, int POL>
 void launch_play_rand(oth_env* env, int n_plies, int32_t* actions, int32_t* rewards, uint8_t* dones, uint64_t ply0,

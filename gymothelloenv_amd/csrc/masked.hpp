@@ -36,9 +36,6 @@
 #ifndef OTH_MS_G
 #define OTH_MS_G 4  // lanes per board up to 128 squares (16 beyond)
 #endif
-#ifndef OTH_MS_NT
-#define OTH_MS_NT 0  // 1: non-temporal logits loads (measured -27 % bandwidth)
-#endif
 
 namespace oth_ms {
 
@@ -127,13 +124,7 @@ __device__ __forceinline__ void load_slot(Slot<CH, G>& b, int l, int NN, const f
         b.nib[bi] = (uint32_t)(b.words[sq >> 6] >> (sq & 63)) & inside;
         if constexpr (VEC) {  // N*N % 4 == 0: a block is all inside or all outside
             f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            if (sq < NN) {
-#if OTH_MS_NT
-                v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(row + sq));
-#else
-                v = *reinterpret_cast<const f32x4*>(row + sq);
-#endif
-            }
+            if (sq < NN) v = *reinterpret_cast<const f32x4*>(row + sq);
             b.x[bi][0] = v.x;
             b.x[bi][1] = v.y;
             b.x[bi][2] = v.z;
@@ -367,30 +358,11 @@ __device__ __forceinline__ void excl_scan_lanes(const float* a, float* r) {
     for (int l = 1; l < G; ++l) r[l] = v[l - 1];
 }
 
-// The logits rows of a wave's 64 consecutive boards (VEC rows: N*N % 4 == 0)
-// staged through LDS: the wave reads the rows as one contiguous stream of
-// 16-byte quads (lane i takes quads i, i+64, ...: every load instruction
-// covers 1 KiB of consecutive rows when ld == N*N) and writes them to `stage`
-// (rows padded by one quad against bank conflicts); then each lane reads its
-// own row.  `stage` holds 64 * (QN + 1) quads for this wave.
-template <int QN>
-__device__ __forceinline__ void stage_rows(f32x4* stage, long long b0, int E, const float* __restrict__ logits,
-                                           long long ld, int lane) {
-#pragma unroll 4
-    for (int k = 0; k < QN; ++k) {
-        const int c = k * 64 + lane;  // quad c of the 64 x QN block
-        const int r = c / QN, q = c - r * QN;
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (b0 + r < E) v = *reinterpret_cast<const f32x4*>(logits + (size_t)(b0 + r) * (size_t)ld + 4 * q);
-        stage[r * (QN + 1) + q] = v;
-    }
-}
-
 template <int CH, int G, bool VEC, bool FULL>
 __device__ __forceinline__ Pick sample_lane(int e, int NN, const float* __restrict__ logits, long long ld,
                                             const uint64_t* __restrict__ legal, const float* __restrict__ uniforms,
                                             uint64_t seed, uint32_t id_base, uint64_t counter, int mode, int a_in,
-                                            bool want_lp, bool want_ent, const f32x4* staged = nullptr) {
+                                            bool want_lp, bool want_ent) {
     constexpr int NB = CH * (16 / G);
     const float* row = logits + (size_t)e * (size_t)ld;
     uint64_t words[CH];
@@ -408,7 +380,7 @@ __device__ __forceinline__ Pick sample_lane(int e, int NN, const float* __restri
             nib[l][bi] = (uint32_t)(words[sq >> 6] >> (sq & 63)) & inside;
             if constexpr (VEC) {
                 f32x4 v = {0.f, 0.f, 0.f, 0.f};
-                if (sq < NN) v = staged ? staged[sq >> 2] : *reinterpret_cast<const f32x4*>(row + sq);
+                if (sq < NN) v = *reinterpret_cast<const f32x4*>(row + sq);
                 x[l][bi][0] = v.x;
                 x[l][bi][1] = v.y;
                 x[l][bi][2] = v.z;

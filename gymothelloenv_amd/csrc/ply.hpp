@@ -1,0 +1,273 @@
+// ply.hpp -- the single-ply kernel of one-word boards (N <= 8): one launch =
+// one OthelloBaseEnv.step (othello.py:412-462) of every board, with the state
+// read from and written back to HBM.  Two sources of the move:
+//   PLY_ACTIONS  the caller's device actions (oth_step: the north-star
+//                step(action) path, any action, legal or not);
+//   PLY_RANDOM   RandomPolicy.get_action (simple_policies.py:37-41) from the
+//                Philox stream (oth_step_policy(RANDOM, n_plies = 1)).
+// Results are identical to k_step / k_play (the generic kernels); the shape is
+// built for a launch that moves every board once:
+//   * every load a lane needs (board, possible_moves, flags, action, the
+//     wave's W/D/L slot) is issued first and unconditionally (lanes past E load
+//     board E - 1 and store nothing), so one memory latency is paid, not two;
+//   * update_board's flips come from a ray table (the handle's 4 KiB table in
+//     device memory, staged in LDS by one 16-byte load per thread issued before
+//     the boards' loads) with the capping test of the nearest non-opponent
+//     square: about 60 VALU and eight LDS reads for the eight directions against
+//     about 260 VALU for Kogge-Stone runs from the square;
+//   * the reset position's possible_moves is a compile-time constant;
+//   * the W/D/L tally is per wave: three ballots, and lane 0 adds their counts
+//     to the wave's own slot with plain stores (read with the board loads) --
+//     no LDS, no barrier, no atomics.
+#pragma once
+
+#include "device.hpp"
+
+namespace oth_dev {
+
+constexpr int PLY_ACTIONS = 0, PLY_RANDOM = 1;
+
+// black's possible_moves on the reset board (_reset_board + get_possible_actions,
+// othello.py:256-263, 313-343), by a compile-time ray walk
+template <int N>
+constexpr uint64_t start_moves() {
+    static_assert(Geo<N>::W == 1, "one-word boards");
+    const uint64_t B = Start<N>::BLACK.w[0], Wt = Start<N>::WHITE.w[0];
+    uint64_t L = 0;
+    for (int a = 0; a < N * N; ++a) {
+        if (((B | Wt) >> a) & 1ull) continue;
+        for (int dr = -1; dr <= 1; ++dr)
+            for (int dc = -1; dc <= 1; ++dc) {
+                if (!dr && !dc) continue;
+                int r = a / N + dr, c = a % N + dc, run = 0;
+                while (r >= 0 && r < N && c >= 0 && c < N && ((Wt >> (r * N + c)) & 1ull)) {
+                    r += dr;
+                    c += dc;
+                    ++run;
+                }
+                if (run > 0 && r >= 0 && r < N && c >= 0 && c < N && ((B >> (r * N + c)) & 1ull)) L |= 1ull << a;
+            }
+    }
+    return L;
+}
+
+// The run one direction flips: the ray's squares before its nearest
+// non-opponent square y0 (the lowest set bit of y = ray & ~O; all of them
+// opponent discs), kept iff y0 holds an own disc.  y - 1 keeps y's higher bits,
+// which are not opponent squares, so ray & O & (y - 1) is exactly that run (the
+// whole ray when y == 0, then uncapped).
+__device__ __forceinline__ uint64_t capped_run(uint64_t ray, uint64_t P, uint64_t O) {
+    const uint64_t y = ray & ~O;
+    const uint64_t ym = y - 1ull;
+    const uint64_t run = and3_64(ray, O, ym);
+    const uint64_t cap = y & ~ym & P;  // y0 if it is an own disc
+    return cap ? run : 0ull;
+}
+
+
+// update_board's flips (othello.py:391-410) for a move on square a: the four
+// directions toward higher squares on the board, the four toward lower ones on
+// the board turned by 180 degrees (OneWord::turn180), where they point to
+// higher squares too.  r = rays + a, the table of fill_rays<N, true>.
+template <int N>
+__device__ __forceinline__ uint64_t flips_rays(uint64_t P, uint64_t O, const uint64_t* __restrict__ r) {
+    uint64_t ray[8];
+#pragma unroll
+    for (int d = 0; d < 8; ++d) ray[d] = r[64 * d];
+    uint64_t f = 0, g = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) f |= capped_run(ray[d], P, O);
+    const uint64_t Pt = OneWord<N>::turn180(P), Ot = OneWord<N>::turn180(O);
+#pragma unroll
+    for (int d = 4; d < 8; ++d) g |= capped_run(ray[d], Pt, Ot);
+    return f | OneWord<N>::turn180(g);
+}
+
+// Per-wave W/D/L slot of a one-lane-per-board launch: slot w of the handle's
+// [nslots][4] array belongs to wave w of the grid (nslots = ceil(E / 64) covers
+// every wave holding a board; a wave past E reads the last live wave's slot and
+// never writes).  The wave's counts accumulate in SGPRs over its boards (three
+// ballots per group of 64) and lane 0 adds them with plain stores at the end.
+// Launches on a stream are ordered, so the read at a launch's start sees every
+// earlier launch's adds.
+struct WaveSlot {
+    unsigned long long* p;
+    unsigned long long v0, v1, v2;
+    uint32_t nb = 0, nd = 0, nw = 0;
+    __device__ __forceinline__ WaveSlot(unsigned long long* wdl, int t, int E) {
+        // wave-uniform: the slot is read by scalar loads into SGPRs (the values
+        // live through the whole kernel; written back by lane 0's vector stores)
+        const int w = __builtin_amdgcn_readfirstlane(min(t >> 6, (E - 1) >> 6));
+        p = wdl + 4 * (size_t)w;
+        const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(p);
+        v0 = a.x;
+        v1 = a.y;
+        v2 = p[2];
+    }
+    // {black wins, draws, white wins} of this wave's lanes (0 / 1 each)
+    __device__ __forceinline__ void count(bool b, bool d, bool w) {
+        nb += (uint32_t)__popcll(__ballot(b));
+        nd += (uint32_t)__popcll(__ballot(d));
+        nw += (uint32_t)__popcll(__ballot(w));
+    }
+    __device__ __forceinline__ void flush() const {
+        if ((nb | nd | nw) && (threadIdx.x & 63) == 0) {
+            ulonglong2 a;
+            a.x = v0 + nb;
+            a.y = v1 + nd;
+            *reinterpret_cast<ulonglong2*>(p) = a;
+            p[2] = v2 + nw;
+        }
+    }
+};
+
+// OthelloBaseEnv.step (othello.py:412-462) on a one-word board held as
+// (black B, white Wt, possible_moves L, meta m): step_lane + finish_step's
+// decisions, branch-free except the pass re-scan (taken by the wave only when
+// one of its lanes passes).  valid: the action is in possible_moves (`a` in
+// [0, N*N) then).  Returns reward / done / winner (0 unless the game ended).
+template <int N>
+__device__ __forceinline__ void step1(uint64_t& B, uint64_t& Wt, uint64_t& L, uint32_t& m, int a, bool valid,
+                                      uint32_t flags, const uint64_t* __restrict__ rays, int& reward, int& done,
+                                      int& winner) {
+    constexpr uint64_t BD = Geo<N>::BOARD.w[0];
+    constexpr int NN = N * N;
+    const bool tw = (m & M_TURN_WHITE) != 0;
+    uint64_t P = tw ? Wt : B, O = tw ? B : Wt;
+    const uint64_t mv = valid ? 1ull << a : 0ull;                          // update_board (:391-410)
+    const uint64_t f = flips_rays<N>(P, O, rays + (a & 63)) & (0ull - (uint64_t)valid);
+    P |= f | mv;
+    O &= ~f;
+    const bool full = (P | O) == BD;                                        // :425-426
+    const bool sudden = !valid && (flags & OTH_SUDDEN_DEATH);              // :427
+    const bool stale = sudden || full;  // :431-433: turn and possible_moves stay as they were
+    uint64_t t[8];
+    uint64_t nl = OneWord<N>::legal(O, P, t);                               // :436
+    const bool opp_pass = nl == 0;
+    if (opp_pass && !stale) nl = OneWord<N>::legal(P, O, t);                // :437-440
+    const bool term = stale || (opp_pass && nl == 0);                       // :441-442
+    const int pc = popc64(P), oc = popc64(O);
+    const int cur = tw ? WHITE_DISK : BLACK_DISK;
+    const int by_count = pc > oc ? cur : (pc < oc ? -cur : NO_DISK);       // determine_winner (:486-501)
+    winner = term ? (sudden ? -cur : by_count) : NO_DISK;                   // :475-485
+    L = stale ? L : nl;
+    Wt = tw ? P : O;
+    B = tw ? O : P;
+    const bool new_tw = (!stale && !opp_pass) ? !tw : tw;
+    int r = 0;  // :444-461
+    if (flags & OTH_DISK_REWARD) r = sudden ? -NN : (oc == 0 ? NN : pc - oc);
+    else r = winner * cur;
+    reward = term ? r : 0;
+    done = term ? 1 : 0;
+    const uint32_t wcode = winner == WHITE_DISK ? 1u : (winner == BLACK_DISK ? 2u : 0u);
+    m = (m & 0xff00u) | (new_tw ? M_TURN_WHITE : 0u) | (term ? M_TERMINATED | (wcode << M_WINNER_SHIFT) : 0u);
+}
+
+// One ply of every board, one lane per board.  A grid-stride loop with the
+// next group's loads issued before the current group's work measured slower
+// (1,048,576 boards: 15.4 -> 16.2 us per ply).
+template <int N, int SRC>
+__device__ __forceinline__ void ply_body(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
+                                         uint64_t* __restrict__ legal, int E, uint32_t flags,
+                                         int32_t* __restrict__ actions, int32_t* __restrict__ rewards,
+                                         uint8_t* __restrict__ dones, unsigned long long* __restrict__ wdl,
+                                         const uint64_t* __restrict__ rays_g, Rng rng, uint64_t ply) {
+    static_assert(Geo<N>::W == 1, "one-word boards");
+    static_assert(BLOCK * 2 == 8 * 64, "one 16-byte piece of the ray table per thread");
+    constexpr int NN = N * N;
+    __shared__ __attribute__((aligned(16))) uint64_t rays[8 * 64];
+    ply += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
+    const int t = blockIdx.x * BLOCK + threadIdx.x;
+    const bool mine = t < E;
+    const int e = mine ? t : E - 1;
+    // every load first, none behind a branch: the ray table's piece first of
+    // all (the wave then waits only for it before its LDS store), the board's
+    // loads (lanes past E load board E - 1 and store nothing), the wave's slot
+    const ulonglong2 rv = reinterpret_cast<const ulonglong2*>(rays_g)[threadIdx.x];
+    const ulonglong2 bw = reinterpret_cast<const ulonglong2*>(boards)[e];
+    uint64_t L = legal[e];
+    uint32_t m = meta[e];
+    int a = 0;
+    if constexpr (SRC == PLY_ACTIONS) a = actions[e];
+    WaveSlot slot(wdl, t, E);
+    reinterpret_cast<ulonglong2*>(rays)[threadIdx.x] = rv;
+    __syncthreads();
+    const uint32_t id = rng.id_base + (uint32_t)e;
+    uint64_t B = bw.x, Wt = bw.y;
+    const bool was_term = (m & M_TERMINATED) != 0;
+    bool valid;
+    if constexpr (SRC == PLY_RANDOM) {
+        // RandomPolicy: possible_moves[randint(len)] (k_play's pick); -1 without a move
+        const uint32_t u = action_draw(rng.seed, id, ply);
+        const int n = popc64(L);
+        a = n ? select64(L, scale_index(u, n)) : -1;
+        a = was_term ? -1 : a;  // k_play: a terminated board reports action -1
+        valid = a >= 0;
+        if (!was_term && (m >> M_RAND_SHIFT) > 0) m -= 1u << M_RAND_SHIFT;  // a random-opening ply used up
+    } else {
+        valid = (unsigned)a < (unsigned)NN && ((L >> (a & 63)) & 1ull);  // `action not in possible_moves` (:417)
+    }
+    int r, d, win;
+    step1<N>(B, Wt, L, m, a, valid, flags, rays, r, d, win);
+    if (was_term) {  // reference: ValueError (othello.py:415-416); batched: a no-op reporting done
+        r = 0;       // (the state is not stored back)
+        d = 1;
+    }
+    const bool ended = mine && d && !was_term;
+    if (ended && (flags & OTH_AUTO_RESET)) {  // reset (othello.py:256-271), black to move
+        B = Start<N>::BLACK.w[0];
+        Wt = Start<N>::WHITE.w[0];
+        constexpr uint64_t START_MOVES = start_moves<N>();  // constant-evaluated
+        L = START_MOVES;
+        uint32_t rl = 0;
+        if (rng.init_rand > 0)
+            rl = (uint32_t)scale_index(philox_x(rng.seed, id, ply, RNG_OPENING_AUTO), rng.init_rand / 2 + 1) * 2u;
+        m = (rl & 0xffu) << M_RAND_SHIFT;
+    }
+    if (mine) {
+        if (!was_term) {
+            ulonglong2 o;
+            o.x = B;
+            o.y = Wt;
+            reinterpret_cast<ulonglong2*>(boards)[e] = o;
+            legal[e] = L;
+            meta[e] = (uint16_t)m;
+        }
+        if constexpr (SRC == PLY_RANDOM)
+            if (actions) actions[e] = a;
+        if (rewards) rewards[e] = r;
+        if (dones) dones[e] = (uint8_t)d;
+    }
+    slot.count(ended && win == BLACK_DISK, ended && win == NO_DISK, ended && win == WHITE_DISK);
+    slot.flush();
+}
+
+// oth_step on one-word boards (no register bound: 64 VGPRs forced a spill,
+// whose scratch traffic cost 16 B per board)
+template <int N>
+__global__ __launch_bounds__(BLOCK) void k_ply_step(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
+                                                    uint64_t* __restrict__ legal, int E, uint32_t flags,
+                                                    const int32_t* __restrict__ actions, int32_t* __restrict__ rewards,
+                                                    uint8_t* __restrict__ dones, unsigned long long* __restrict__ wdl,
+                                                    const uint64_t* __restrict__ rays, Rng rng, uint64_t ply) {
+    ply_body<N, PLY_ACTIONS>(boards, meta, legal, E, flags, const_cast<int32_t*>(actions), rewards, dones, wdl, rays,
+                             rng, ply);
+}
+
+// oth_step_policy(RANDOM, 1 ply) on one-word boards
+template <int N>
+__global__ __launch_bounds__(BLOCK) void k_ply_rand(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
+                                                    uint64_t* __restrict__ legal, int E, uint32_t flags,
+                                                    int32_t* __restrict__ actions, int32_t* __restrict__ rewards,
+                                                    uint8_t* __restrict__ dones, unsigned long long* __restrict__ wdl,
+                                                    const uint64_t* __restrict__ rays, Rng rng, uint64_t ply) {
+    ply_body<N, PLY_RANDOM>(boards, meta, legal, E, flags, actions, rewards, dones, wdl, rays, rng, ply);
+}
+
+// oth_create: the handle's ray table (fill_rays<N, true>'s layout) in device memory
+template <int N>
+__global__ __launch_bounds__(BLOCK) void k_fill_rays(uint64_t* __restrict__ rays) {
+    fill_rays<N, true, false>(rays);
+}
+
+}  // namespace oth_dev

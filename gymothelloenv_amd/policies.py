@@ -70,11 +70,13 @@ class GreedyPolicy(object):
 
 
 class MaxiMinPolicy(object):
-    """simple_policies.py:98-163 (max_search_depth 1..3), searched on the device."""
+    """simple_policies.py:98-163, searched on the device (max_search_depth 1 ..
+    OTH_MAXIMIN_MAX_DEPTH = 10; the reference's search is exponential in the depth)."""
 
     def __init__(self, max_search_depth=1):
-        if not 1 <= int(max_search_depth) <= 3:
-            raise ValueError("max_search_depth must be 1, 2 or 3 on the device")
+        from ._lib import OTH_MAXIMIN_MAX_DEPTH
+        if not 1 <= int(max_search_depth) <= OTH_MAXIMIN_MAX_DEPTH:
+            raise ValueError("max_search_depth must be in 1 .. %d on the device" % OTH_MAXIMIN_MAX_DEPTH)
         self.env = None
         self.max_search_depth = int(max_search_depth)
 
@@ -85,9 +87,7 @@ class MaxiMinPolicy(object):
         vec = self.env._vec
         self.env._sync()
         a = int(vec.policy_actions("maximin%d" % self.max_search_depth).cpu()[0])
-        if a < 0:
-            raise ValueError('no possible moves')
-        return a
+        return a if a >= 0 else None  # the reference's search returns no move then (:117-126, :157-163)
 
     def get_test_action(self, obs):
         return self.get_action(obs)

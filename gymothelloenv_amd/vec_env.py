@@ -20,9 +20,8 @@ _OBS_LAYOUTS = {"board": L.OTH_OBS_BOARD, "board_legal": L.OTH_OBS_BOARD_LEGAL,
 _OBS_PLANES = {L.OTH_OBS_BOARD: 1, L.OTH_OBS_BOARD_LEGAL: 2, L.OTH_OBS_MAKE_STATE: 4, L.OTH_OBS_ABSOLUTE: 1}
 _DTYPES = {torch.int8: L.OTH_I8, torch.int32: L.OTH_I32, torch.int64: L.OTH_I64,
            torch.float32: L.OTH_F32, torch.float64: L.OTH_F64}
-_POLICIES = {"random": L.OTH_POLICY_RANDOM, "greedy": L.OTH_POLICY_GREEDY,
-             "maximin1": L.OTH_POLICY_MAXIMIN1, "maximin2": L.OTH_POLICY_MAXIMIN2,
-             "maximin3": L.OTH_POLICY_MAXIMIN3}
+_POLICIES = {"random": L.OTH_POLICY_RANDOM, "greedy": L.OTH_POLICY_GREEDY}
+_POLICIES.update({"maximin%d" % d: L.OTH_POLICY_MAXIMIN(d) for d in range(1, L.OTH_MAXIMIN_MAX_DEPTH + 1)})
 
 BLACK_DISK, NO_DISK, WHITE_DISK = -1, 0, 1  # othello.py:10-12
 
@@ -54,6 +53,8 @@ class VecOthelloEnv(object):
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:  # "cuda" -> the current device, by index
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.num_envs = int(num_envs)
         self.board_size = max(4, int(board_size))  # othello.py:230
         self.words = nwords(self.board_size)
@@ -287,6 +288,22 @@ class VecOthelloEnv(object):
         L.check(self._lib.oth_counts_vs(self._h, _ptr(out), int(bool(reset)), self._stream()), "oth_counts_vs")
         return out
 
+    def _sampler_inputs(self, logits, uniforms):
+        """(logits rows, uniforms) checked before a launch reads them: the rows on
+        this handle's device, one per board; uniforms float32 on it, >= E of them."""
+        x = _rows(logits, self.board_size)
+        if x.device != self.device:
+            raise ValueError("logits must be on %s (got %s)" % (self.device, x.device))
+        if x.shape[0] != self.num_envs:
+            raise ValueError("logits must have one row per board")
+        if uniforms is not None:
+            if uniforms.dtype != torch.float32 or not uniforms.is_contiguous() or uniforms.device != self.device:
+                uniforms = uniforms.to(device=self.device, dtype=torch.float32).contiguous()
+            if uniforms.numel() < self.num_envs:
+                raise ValueError("uniforms must hold one value per board (%d), got %d" %
+                                 (self.num_envs, uniforms.numel()))
+        return x, uniforms
+
     def sample_actions(self, logits, deterministic=False, uniforms=None, log_probs=True, entropy=True):
         """Policy.act (model.py:60-99) for every board at once: sample (or, when
         deterministic, take the mode of) the softmax of `logits` (E, N*N)
@@ -294,12 +311,7 @@ class VecOthelloEnv(object):
         keyed (seed, env id, call counter) unless `uniforms` (E,) is given.
         Returns (actions int32, log_probs, entropy) on the device; the actions
         feed step() directly."""
-        from .masked import _rows
-        x = _rows(logits, self.board_size)
-        if x.shape[0] != self.num_envs:
-            raise ValueError("logits must have one row per board")
-        if uniforms is not None:
-            uniforms = uniforms.to(device=x.device, dtype=torch.float32).contiguous()
+        x, uniforms = self._sampler_inputs(logits, uniforms)
         acts = self._i32(self.num_envs)
         lp = torch.empty(self.num_envs, dtype=torch.float32, device=self.device) if log_probs else None
         ent = torch.empty(self.num_envs, dtype=torch.float32, device=self.device) if entropy else None
@@ -319,12 +331,7 @@ class VecOthelloEnv(object):
         Outputs may be given to be written in place: `actions` / `rewards` int32 (E,),
         `dones` uint8 (E,), and `log_probs` / `entropy` as float32 (E,) tensors
         instead of True."""
-        x = _rows(logits, self.board_size)
-        if x.shape[0] != self.num_envs:
-            raise ValueError("logits must have one row per board")
-        if uniforms is not None and (uniforms.dtype != torch.float32 or not uniforms.is_contiguous() or
-                                     uniforms.device != x.device):
-            uniforms = uniforms.to(device=x.device, dtype=torch.float32).contiguous()
+        x, uniforms = self._sampler_inputs(logits, uniforms)
         acts = self._out(actions, torch.int32, "actions")
         lp = self._out(log_probs, torch.float32, "log_probs")
         ent = self._out(entropy, torch.float32, "entropy")
@@ -336,7 +343,7 @@ class VecOthelloEnv(object):
                                           _ptr(acts), _ptr(lp), _ptr(ent), _ptr(r), _ptr(d), self._stream()),
                 "oth_sample_step")
         self._sample_calls += 1
-        return acts, lp, ent, r, d.view(torch.bool)
+        return acts, lp, ent, r, (d.view(torch.bool) if d is not None else None)
 
     @property
     def sample_counter(self):
@@ -369,7 +376,9 @@ class VecOthelloEnv(object):
         so replay r draws counters base + r*d .. base + r*d + d - 1: fresh
         Philox numbers every replay (random openings, device opponents,
         sample_actions without uniforms), disjoint from eager calls and from
-        every other region of this handle.  Yields the slot.
+        every other region of this handle.  Yields the slot.  A region that
+        fails gives its slot back; a captured graph keeps it until
+        release_graph_slot(slot) (call it when the graph is dropped).
 
             with torch.cuda.graph(g), env.graph_region() as slot:
                 for k in range(K): env.step(env.sample_actions(actor(obs))[0]); ...
@@ -393,14 +402,28 @@ class VecOthelloEnv(object):
             d_ply = ctypes.c_uint64()
             rc = self._lib.oth_graph_end(self._h, d_smp, int(capturing), ctypes.byref(d_ply), self._stream())
             resets, self._region_resets = self._region_resets, None
-            if ok:
-                L.check(rc, "oth_graph_end")
-                if not capturing:
-                    raise RuntimeError("the capture ended inside graph_region: enter graph_region inside "
-                                       "torch.cuda.graph(...), not around it")
-                if resets and self.initial_rand_steps > 0 and d_ply.value == 0:
-                    raise RuntimeError("this graph region only resets boards with random openings: every replay "
-                                       "would draw the same openings; capture at least one ply with the reset")
+            try:
+                if ok:
+                    L.check(rc, "oth_graph_end")
+                    if not capturing:
+                        raise RuntimeError("the capture ended inside graph_region: enter graph_region inside "
+                                           "torch.cuda.graph(...), not around it")
+                    if resets and self.initial_rand_steps > 0 and d_ply.value == 0:
+                        raise RuntimeError("this graph region only resets boards with random openings: every "
+                                           "replay would draw the same openings; capture at least one ply with "
+                                           "the reset")
+            except BaseException:
+                ok = False
+                raise
+            finally:
+                if not ok:  # no usable graph: the slot goes back
+                    self._lib.oth_graph_release(self._h, k)
+
+    def release_graph_slot(self, slot):
+        """Give a graph region's counter slot back once its graph is dropped
+        (oth_graph_release); the slot's offsets are kept, so a later region on
+        it still draws counters no earlier replay drew."""
+        L.check(self._lib.oth_graph_release(self._h, int(slot)), "oth_graph_release")
 
     def state_dict(self):
         """Boards, meta, possible_moves and the eager counters (host values).

@@ -55,7 +55,8 @@ enum {
 };
 
 /* on-device scripted policies (simple_policies.py): RandomPolicy, GreedyPolicy,
- * MaxiMinPolicy(max_search_depth = 1, 2, 3); MAXIMIN1 plays exactly GREEDY's moves */
+ * MaxiMinPolicy(max_search_depth = d) for d = 1 .. OTH_MAXIMIN_MAX_DEPTH as
+ * OTH_POLICY_MAXIMIN(d); MAXIMIN1 plays exactly GREEDY's moves */
 enum {
     OTH_POLICY_RANDOM = 0,
     OTH_POLICY_GREEDY = 1,
@@ -63,6 +64,9 @@ enum {
     OTH_POLICY_MAXIMIN2 = 3,
     OTH_POLICY_MAXIMIN3 = 4
 };
+#define OTH_MAXIMIN_MAX_DEPTH 10
+#define OTH_POLICY_MAXIMIN(d) (OTH_POLICY_MAXIMIN1 + (d) - 1)
+#define OTH_POLICY_LAST OTH_POLICY_MAXIMIN(OTH_MAXIMIN_MAX_DEPTH)
 
 /* observation layouts */
 enum {
@@ -148,7 +152,7 @@ int oth_legal_moves(int32_t board_size, int32_t n, const uint64_t *mover, const 
 int oth_greedy_actions(oth_env *env, int32_t *out, oth_stream_t stream);
 
 /* The move of a deterministic scripted policy (OTH_POLICY_GREEDY or
- * OTH_POLICY_MAXIMIN1..3: MaxiMinPolicy.get_action, simple_policies.py:157-163)
+ * OTH_POLICY_MAXIMIN(d): MaxiMinPolicy(d).get_action, simple_policies.py:157-163)
  * for the side to move in every env; -1 where possible_moves is empty. */
 int oth_policy_actions(oth_env *env, int32_t policy, int32_t *out, oth_stream_t stream);
 
@@ -239,12 +243,16 @@ int oth_set_ply_counter(oth_env *env, uint64_t ply);
  *     range must start at k << SHIFT as well.
  *   oth_graph_offsets: slot k's (ply, sample) offsets; synchronises the device
  *     (never call it while a capture is active).
+ *   oth_graph_release: gives slot k back (its graph is dropped, or its capture
+ *     failed); oth_graph_begin hands out the lowest free slot.  The slot's
+ *     offsets are kept, so a later region on it still draws fresh counters.
  * Eager launches use slot 0, always 0. */
 #define OTH_GRAPH_SLOTS 64
 #define OTH_GRAPH_COUNTER_SHIFT 40
 int oth_graph_begin(oth_env *env, int32_t *slot);
 int oth_graph_end(oth_env *env, uint64_t d_sample, int32_t enqueue, uint64_t *d_ply, oth_stream_t stream);
 int oth_graph_offsets(const oth_env *env, int32_t slot, uint64_t out[2]);
+int oth_graph_release(oth_env *env, int32_t slot);
 
 /* Handle geometry: n_envs, board_size, W. */
 int oth_shape(const oth_env *env, int32_t *n_envs, int32_t *board_size, int32_t *words);

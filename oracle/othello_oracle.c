@@ -220,7 +220,7 @@ static int greedy_action(const oenv *e) {
 
 static int maximin_search(const oenv *e, int depth, int max_depth, int perspective, int my, int *move);
 
-/* the move of a deterministic scripted policy: 1 GreedyPolicy, 2..4 MaxiMinPolicy(1..3) */
+/* the move of a deterministic scripted policy: 1 GreedyPolicy, 2.. MaxiMinPolicy(policy - 1), any depth */
 static int policy_move(const oenv *e, int policy) {
     int mv;
     if (policy == 1) return greedy_action(e);
@@ -389,7 +389,7 @@ void oracle_reset_openings(int n, int E, uint64_t seed, uint32_t id_base, uint64
 }
 
 /* On-device-policy rollout semantics (oth_step_policy): `plies` plies over E
- * envs.  policy 0 = random, 1 = greedy, 2..4 = maximin depth 1..3.  Global ply index g = ply0 + p.
+ * envs.  policy 0 = random, 1 = greedy, d + 1 = maximin depth d.  Global ply index g = ply0 + p.
  * actions/rewards/dones are [plies][E] (NULL to skip); wdl[3] accumulates
  * {black wins, draws, white wins} over games that end in this call. */
 int oracle_rollout(int n, uint32_t flags, int policy, int initial_rand_steps, uint64_t seed, uint32_t id_base,

@@ -419,6 +419,39 @@ def gen_maximin(othello, simple_policies):
     np.savez_compressed(os.path.join(OUT, "maximin.npz"), **out)
 
 
+def gen_maximin_deep(othello, simple_policies):
+    """MaxiMinPolicy(depth) beyond depth 3 (simple_policies.py:98-163): depth 4
+    at N = 6 and 8, depth 5 at N = 6, on positions from random play (the
+    reference's search is exponential in the depth, so fewer positions)."""
+    out = {}
+    for n, depth, positions in ((6, 4, 40), (6, 5, 20), (8, 4, 16)):
+        rnd = np.random.RandomState(97 * n + depth)
+        env = othello.OthelloBaseEnv(board_size=n, mute=True)
+        pol = simple_policies.MaxiMinPolicy(depth)
+        pol.reset(env)
+        blacks, whites, turns, acts = [], [], [], []
+        while len(acts) < positions:
+            env.reset()
+            done = False
+            while not done and len(acts) < positions:
+                if rnd.rand() < 0.25:
+                    a = pol.get_action(env.get_observation())
+                    b, w, t, _ = snapshot(env, n)
+                    blacks.append(b)
+                    whites.append(w)
+                    turns.append(t)
+                    acts.append(int(a))
+                pm = env.possible_moves
+                _, _, done, _ = env.step(int(pm[rnd.randint(0, len(pm))]))
+        key = "N%d_d%d_" % (n, depth)
+        out[key + "black"] = np.array(blacks, dtype=np.uint64)
+        out[key + "white"] = np.array(whites, dtype=np.uint64)
+        out[key + "turn"] = np.array(turns, dtype=np.int8)
+        out[key + "action"] = np.array(acts, dtype=np.int32)
+        print("maximin N=%d depth=%d: %d positions" % (n, depth, len(acts)), flush=True)
+    np.savez_compressed(os.path.join(OUT, "maximin_deep.npz"), **out)
+
+
 def install_learner_shims():
     """Stand-ins for what the learners' modules import but the policy heads never
     use: torch.utils.tensorboard (ppo.py:7; tensorboard is absent), the
@@ -553,6 +586,9 @@ def main():
     if sys.argv[1:] == ["masked"]:
         gen_masked(othello)
         return
+    if sys.argv[1:] == ["maximin_deep"]:
+        gen_maximin_deep(othello, simple_policies)
+        return
     gen_kat(othello)
     gen_trajectories(othello)
     gen_greedy(othello, simple_policies, util)
@@ -560,6 +596,7 @@ def main():
     gen_wrappers(othello, simple_policies)
     gen_vs(othello)
     gen_maximin(othello, simple_policies)
+    gen_maximin_deep(othello, simple_policies)
     gen_masked(othello)
 
 

@@ -58,6 +58,20 @@ def test_spawned_ranks_cover_the_global_boards(world):
         assert base == nxt and n == 131072
         nxt += n
     assert nxt == d["global_envs"]
+    # the record's keys at N > 1 (numbers are null in a dry run): the scaling reading aids
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "roofline", "config",
+              "per_gpu_value", "single_gpu_same_shard", "ranks", "shared_device"):
+        assert k in d, k
+    assert d["n_gpus"] == world and d["ranks"] == world and d["shared_device"] is False
+    assert d["config"]["boards_per_gpu"] == 131072 and d["roofline"]["bound"] == "hbm"
+
+
+def test_shared_device_rehearsal_is_labelled():
+    """Ranks pinned to one device (OTH_BENCH_DEVICE) report one distinct GPU."""
+    r = _run(["--gpus", "2", "--dry-run"], env_extra={"OTH_BENCH_DEVICE": "0"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["shared_device"] is True and d["n_gpus"] == 1 and d["ranks"] == 2
 
 
 def test_world_size_mismatch_fails():

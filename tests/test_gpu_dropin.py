@@ -156,10 +156,10 @@ def test_greedy_policy_and_make_state(pkg, golden_dir, n):
 
 
 def test_maximin_policy_dropin(pkg, golden_dir):
-    g = np.load(os.path.join(golden_dir, "maximin.npz"))
     env = pkg.OthelloBaseEnv(board_size=8, mute=True)
     env.reset()
-    for depth in (1, 2, 3):
+    for depth in (1, 2, 3, 4):
+        g = np.load(os.path.join(golden_dir, "maximin.npz" if depth <= 3 else "maximin_deep.npz"))
         pol = pkg.MaxiMinPolicy(depth)
         pol.reset(env)
         k = "N8_d%d_" % depth

@@ -205,6 +205,45 @@ def test_graph_region_misuse_raises(torch_gpu):
     assert env.ply_counter == 0
     env.step_policy("random", n_plies=3)
     assert env.ply_counter == 3
+    # the refused region gave its slot back: the next region gets slot 1
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g), env.graph_region() as slot:
+        env.step_policy("random", n_plies=1)
+    assert slot == 1
+
+
+def test_graph_slots_exhaust_and_release(torch_gpu):
+    """63 captured regions take every counter slot; the next region is refused
+    with a clear error and leaves the handle usable; a released slot is handed
+    out again and its replays still draw counters no earlier replay drew."""
+    torch = torch_gpu
+    from gymothelloenv_amd import VecOthelloEnv, OthelloLibError
+    env = VecOthelloEnv(256, board_size=8, auto_reset=True, device="cuda:0")
+    graphs, slots = [], []
+    for _ in range(63):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g), env.graph_region() as slot:
+            env.step_policy("random", n_plies=2, record=False)
+        graphs.append(g)
+        slots.append(slot)
+    assert sorted(slots) == list(range(1, 64))
+    with pytest.raises(OthelloLibError, match="no graph counter slot left"):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g), env.graph_region():
+            env.step_policy("random", n_plies=1, record=False)
+    torch.cuda.synchronize()
+    graphs[9].replay()
+    torch.cuda.synchronize()
+    assert env.graph_offsets(10) == (2, 0)
+    env.release_graph_slot(10)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g), env.graph_region() as slot:
+        env.step_policy("random", n_plies=3, record=False)
+    assert slot == 10
+    g.replay()
+    torch.cuda.synchronize()
+    assert env.graph_offsets(10) == (5, 0)  # past the released graph's replay: no counter drawn twice
+    env.step_policy("random", n_plies=1)  # eager plies still run
 
 
 def test_graph_region_step_vs_random_opponent(torch_gpu):

@@ -360,6 +360,22 @@ def test_sample_step_writes_given_outputs(torch_gpu):
         a.sample_step(logits, actions=torch.empty(E, dtype=torch.int64, device=dev))
     with pytest.raises(ValueError):
         a.sample_step(logits, log_probs=torch.empty(E - 1, device=dev))
+    # outputs switched off: nothing returned for them, the step still happens
+    ref = b.sample_step(logits)
+    out = a.sample_step(logits, dones=False, rewards=False)
+    assert out[3] is None and out[4] is None
+    assert torch.equal(out[0], ref[0]) and torch.equal(out[1], ref[1])
+    for x, y in zip(a.get_state(), b.get_state()):
+        assert torch.equal(x, y)
+    # inputs a launch would read out of place are refused before it
+    with pytest.raises(ValueError):
+        a.sample_step(logits.cpu())
+    with pytest.raises(ValueError):
+        a.sample_actions(logits.cpu())
+    with pytest.raises(ValueError):
+        a.sample_step(logits, uniforms=torch.rand(E - 1, device=dev))
+    with pytest.raises(ValueError):
+        a.sample_actions(logits, uniforms=torch.rand(E - 1, device=dev))
 
 
 @pytest.mark.parametrize("n_board,E", [(8, 2049), (8, 40000), (7, 40000), (6, 20000), (10, 5001)])

@@ -454,11 +454,12 @@ def test_vs_rollout_replays_on_oracle(torch_cuda, n, opp, init_rand):
     np.testing.assert_array_equal(env.counts().cpu().numpy(), wdl)
 
 
-@pytest.mark.parametrize("n,depth", [(6, 1), (6, 2), (6, 3), (8, 1), (8, 2), (8, 3)])
+@pytest.mark.parametrize("n,depth", [(6, 1), (6, 2), (6, 3), (8, 1), (8, 2), (8, 3), (6, 4), (6, 5), (8, 4)])
 def test_maximin_actions_match_reference(torch_cuda, golden_dir, n, depth):
-    """MaxiMinPolicy(depth).get_action (simple_policies.py:98-163) on device."""
+    """MaxiMinPolicy(depth).get_action (simple_policies.py:98-163) on device;
+    depth >= 4 runs the explicit-stack search (maximin_search)."""
     torch = torch_cuda
-    g = np.load(os.path.join(golden_dir, "maximin.npz"))
+    g = np.load(os.path.join(golden_dir, "maximin.npz" if depth <= 3 else "maximin_deep.npz"))
     k = "N%d_d%d_" % (n, depth)
     b, w, t, a = g[k + "black"], g[k + "white"], g[k + "turn"], g[k + "action"]
     env = make_env(torch, len(a), n)
@@ -469,7 +470,8 @@ def test_maximin_actions_match_reference(torch_cuda, golden_dir, n, depth):
     np.testing.assert_array_equal(env.policy_actions("maximin%d" % depth).cpu().numpy(), a)
 
 
-@pytest.mark.parametrize("n,policy,pid", [(8, "maximin2", 3), (6, "maximin3", 4), (10, "maximin2", 3)])
+@pytest.mark.parametrize("n,policy,pid", [(8, "maximin2", 3), (6, "maximin3", 4), (10, "maximin2", 3),
+                                          (6, "maximin4", 5), (5, "maximin5", 6)])
 def test_maximin_rollout_replays_on_oracle(torch_cuda, n, policy, pid):
     torch = torch_cuda
     E, plies = 512, 70

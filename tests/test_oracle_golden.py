@@ -178,9 +178,9 @@ def test_vs_greedy_matches_reference(golden_dir, n):
                 assert plies[0] >= 1
 
 
-@pytest.mark.parametrize("n,depth", [(6, 1), (6, 2), (6, 3), (8, 1), (8, 2), (8, 3)])
+@pytest.mark.parametrize("n,depth", [(6, 1), (6, 2), (6, 3), (8, 1), (8, 2), (8, 3), (6, 4), (6, 5), (8, 4)])
 def test_maximin_matches_reference(golden_dir, n, depth):
-    g = np.load(os.path.join(golden_dir, "maximin.npz"))
+    g = np.load(os.path.join(golden_dir, "maximin.npz" if depth <= 3 else "maximin_deep.npz"))
     k = "N%d_d%d_" % (n, depth)
     b, w, t, a = g[k + "black"], g[k + "white"], g[k + "turn"], g[k + "action"]
     s = oracle.State(n, len(a))
