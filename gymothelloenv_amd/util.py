@@ -9,8 +9,6 @@ kernel (OTH_OBS_MAKE_STATE); any other `obs` (a stored or earlier observation)
 is converted by the same formula on the host, as the reference does, since
 the planes then depend on an array the device does not hold.
 """
-import copy
-
 import numpy as np
 import torch
 
@@ -20,27 +18,23 @@ def _base(env):
 
 
 def _make_state_host(obs, player_turn, possible_moves):
-    """util.py:48-74 on an arbitrary obs (the reference's quirks included:
-    the legal plane only with >= 2 moves, size = len(obs))."""
-    moves_number = np.array(possible_moves)
-    size = len(obs)
-    idx1 = moves_number // size
-    idx2 = moves_number % size
+    """util.py:48-74's planes for an arbitrary obs, restated with np.where:
+    the mover's (+1) and the opponent's (-1) entries split into the black and
+    white planes by whose turn it is, the turn plane (0 black / 1 white), and
+    the possible-moves plane -- set only when there are at least two moves
+    (util.py:55), rows indexed by move // len(obs) as the reference does."""
+    obs = np.asarray(obs)
+    # keep: the plane of the side whose discs are +1 (opponent's -1 -> 0);
+    # flip: the other side's (+1 -> 0, then -1 -> 1), values other than +-1 kept
+    keep = np.where(obs == -1, 0, obs).astype(obs.dtype)
+    flip = np.where(obs == 1, 0, np.where(obs == -1, 1, obs)).astype(obs.dtype)
+    black_to_move = player_turn == -1
+    black, white = (keep, flip) if black_to_move else (flip, keep)
+    turn = np.zeros(obs.shape) if black_to_move else np.ones(obs.shape)
+    moves = np.asarray(possible_moves, dtype=np.int64)
     legal = np.zeros(obs.shape)
-    if len(idx1) > 0 and len(idx2) > 1:
-        legal[idx1, idx2] = 1
-    black = copy.deepcopy(obs)
-    white = copy.deepcopy(obs)
-    if player_turn == -1:
-        turn = np.zeros(obs.shape)
-        black[black == -1] = 0
-        white[white == 1] = 0
-        white[white == -1] = 1
-    else:
-        turn = np.ones(obs.shape)
-        black[black == 1] = 0
-        black[black == -1] = 1
-        white[white == -1] = 0
+    if moves.size >= 2:
+        legal[moves // len(obs), moves % len(obs)] = 1
     return np.stack([black, white, turn, legal])
 
 
@@ -55,8 +49,8 @@ def make_state(obs, env):
 
 
 def undo_state(state, player_turn):
-    """util.py:77-85"""
+    """util.py:77-85: the mover-perspective board back from the black and
+    white planes (the turn plane must match player_turn)."""
     assert int((player_turn + 1) / 2) == int(state[2][0][0])
-    if player_turn == -1:
-        return state[0] - state[1]
-    return state[1] - state[0]
+    mine, theirs = (state[0], state[1]) if player_turn == -1 else (state[1], state[0])
+    return mine - theirs

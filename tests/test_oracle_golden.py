@@ -190,3 +190,25 @@ def test_maximin_matches_reference(golden_dir, n, depth):
     np.testing.assert_array_equal(oracle.maximin(s, depth), a)
     if depth == 1:  # MaxiMin-1 == Greedy (README.md:48: identical rows)
         np.testing.assert_array_equal(oracle.greedy(s), a)
+
+
+@pytest.mark.parametrize("n", [6, 8])
+def test_host_make_state_matches_reference(golden_dir, n):
+    """The drop-in's host make_state / undo_state (gymothelloenv_amd/util.py, used
+    for an obs that is not the env's current one) against the reference's
+    util.make_state planes (util.py:48-85), including the legal plane left empty
+    with a single possible move (util.py:55); float64 like the reference."""
+    from gymothelloenv_amd.util import _make_state_host, undo_state
+    o = np.load(os.path.join(golden_dir, "obs.npz"))
+    obs, turn, legal = o["N%d_obs" % n].astype(np.int64), o["N%d_turn" % n], o["N%d_legal" % n]
+    want = o["N%d_make_state" % n]
+    singles = 0
+    for i in range(len(turn)):
+        moves = [a for a in range(n * n) if (int(legal[i][a // 64]) >> (a % 64)) & 1]
+        singles += len(moves) == 1
+        st = _make_state_host(obs[i], int(turn[i]), moves)
+        assert st.dtype == np.float64 and st.shape == (4, n, n)
+        np.testing.assert_array_equal(st, want[i].astype(np.float64))
+        back = undo_state(st, int(turn[i]))
+        np.testing.assert_array_equal(back, obs[i])
+    assert singles > 0  # the >= 2 quirk is exercised
