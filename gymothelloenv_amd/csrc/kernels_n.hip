@@ -65,9 +65,14 @@ template <int N>
 int launch_step(oth_env* env, const int32_t* actions, int32_t* rewards, uint8_t* dones, uint64_t ply,
                 hipStream_t st) {
     if constexpr (Geo<N>::W == 1) {  // the single-ply kernel (ply.hpp)
-        hipLaunchKernelGGL((k_ply_step<N>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards, env->meta,
-                           env->legal, env->E, env->flags, actions, rewards, dones, env->wdl, env->rays, rng_of(env),
-                           ply);
+        if (env->E <= OTH_PLY_MATH_MAX_E)
+            hipLaunchKernelGGL((k_ply_step<N, RAYS_MATH>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards,
+                               env->meta, env->legal, env->E, env->flags, actions, rewards, dones, env->wdl, env->rays,
+                               rng_of(env), ply);
+        else
+            hipLaunchKernelGGL((k_ply_step<N, RAYS_LDS>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards,
+                               env->meta, env->legal, env->E, env->flags, actions, rewards, dones, env->wdl, env->rays,
+                               rng_of(env), ply);
         return after_launch("oth_step");
     }
     hipLaunchKernelGGL(k_step<N>, dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards, env->meta, env->legal,
@@ -83,9 +88,14 @@ void launch_k_play(int lanes_per_board, oth_env* env, int policy, int n_plies, i
     const dim3 grid(grid_for((long long)lanes_per_board * env->E)), block(BLOCK);
     if constexpr (POL == OTH_POLICY_RANDOM && Geo<N>::W == 1) {
         if (n_plies == 1) {  // one ply per launch: the single-ply kernel (ply.hpp), any flags
-            hipLaunchKernelGGL((k_ply_rand<N>), dim3(grid_for(env->E)), block, 0, st, env->boards, env->meta,
-                               env->legal, env->E, env->flags, actions, rewards, dones, env->wdl, env->rays,
-                               rng_of(env), ply0);
+            if (env->E <= OTH_PLY_MATH_MAX_E)
+                hipLaunchKernelGGL((k_ply_rand<N, RAYS_MATH>), dim3(grid_for(env->E)), block, 0, st, env->boards,
+                                   env->meta, env->legal, env->E, env->flags, actions, rewards, dones, env->wdl,
+                                   env->rays, rng_of(env), ply0);
+            else
+                hipLaunchKernelGGL((k_ply_rand<N, RAYS_LDS>), dim3(grid_for(env->E)), block, 0, st, env->boards,
+                                   env->meta, env->legal, env->E, env->flags, actions, rewards, dones, env->wdl,
+                                   env->rays, rng_of(env), ply0);
             return;
         }
     }

@@ -51,6 +51,45 @@ constexpr uint64_t start_moves() {
     return L;
 }
 
+// Where the flips' rays come from (a template parameter of the single-ply kernels):
+//   RAYS_LDS   the handle's table staged in LDS (fewest VALU: faster where the
+//              launch is bandwidth-bound, 1,048,576 boards 15.8 -> 14.9 us per ply)
+//   RAYS_MATH  computed per move, no table, no LDS, no barrier (+32 VALU: faster
+//              where one wave per SIMD runs a latency-bound chain, 65,536
+//              boards 3.37 -> 3.11 us per ply; profiles/r03/ab/ab_blocks.jsonl)
+constexpr int RAYS_LDS = 1, RAYS_MATH = 2;
+#ifndef OTH_PLY_MATH_MAX_E
+#define OTH_PLY_MATH_MAX_E 65536  // single-ply launches of at most this many boards compute their rays
+#endif
+
+// Without a table: the rays of square s toward higher squares (E, S, SE, SW)
+// as one shifted constant each -- the ray from square 0 (or row 0's squares
+// 1 .. N-1 for E) moved to s -- with the squares that wrapped past the board's
+// right (E, SE) or left (SW) edge masked off by column.
+template <int N>
+struct RayMath {
+    static constexpr uint64_t sum_steps(int step, int k0, int k1) {
+        uint64_t x = 0;
+        for (int k = k0; k <= k1; ++k) x |= 1ull << (k * step);
+        return x;
+    }
+    static constexpr uint64_t BD = Geo<N>::BOARD.w[0];
+    static constexpr uint64_t ROW1 = sum_steps(N, 0, N - 1);      // column 0 of every row
+    static constexpr uint64_t EAST = ((1ull << N) - 1) & ~1ull;    // squares 1 .. N-1 of row 0
+    static constexpr uint64_t COL = sum_steps(N, 1, N - 1);       // S from square 0
+    static constexpr uint64_t DIAG = sum_steps(N + 1, 1, N - 1);  // SE from square 0
+    static constexpr uint64_t ANTI = sum_steps(N - 1, 1, N - 1);  // SW from square N-1, moved to square 0
+    __device__ __forceinline__ static void up(uint32_t s, uint32_t c, uint64_t* ray) {
+        const uint32_t row = (1u << N) - 1u;
+        const uint64_t gt = ROW1 * (uint64_t)((row << (c + 1)) & row);  // columns > c of every row
+        const uint64_t lt = ROW1 * (uint64_t)((1u << c) - 1u);           // columns < c
+        ray[0] = (EAST << s) & gt;
+        ray[1] = (COL << s) & BD;
+        ray[2] = (DIAG << s) & gt & BD;
+        ray[3] = (ANTI << s) & lt & BD;
+    }
+};
+
 // The run one direction flips: the ray's squares before its nearest
 // non-opponent square y0 (the lowest set bit of y = ray & ~O; all of them
 // opponent discs), kept iff y0 holds an own disc.  y - 1 keeps y's higher bits,
@@ -69,11 +108,17 @@ __device__ __forceinline__ uint64_t capped_run(uint64_t ray, uint64_t P, uint64_
 // directions toward higher squares on the board, the four toward lower ones on
 // the board turned by 180 degrees (OneWord::turn180), where they point to
 // higher squares too.  r = rays + a, the table of fill_rays<N, true>.
-template <int N>
-__device__ __forceinline__ uint64_t flips_rays(uint64_t P, uint64_t O, const uint64_t* __restrict__ r) {
+template <int N, int RAYS>
+__device__ __forceinline__ uint64_t flips_rays(uint64_t P, uint64_t O, const uint64_t* __restrict__ r, int a) {
     uint64_t ray[8];
+    if constexpr (RAYS == RAYS_MATH) {  // the turned rays are the up rays of square NN-1-a, column N-1-c
+        const uint32_t s = (uint32_t)a & 63u, c = s % N;
+        RayMath<N>::up(s, c, ray);
+        RayMath<N>::up(N * N - 1 - s, N - 1 - c, ray + 4);
+    } else {
 #pragma unroll
-    for (int d = 0; d < 8; ++d) ray[d] = r[64 * d];
+        for (int d = 0; d < 8; ++d) ray[d] = r[64 * d];
+    }
     uint64_t f = 0, g = 0;
 #pragma unroll
     for (int d = 0; d < 4; ++d) f |= capped_run(ray[d], P, O);
@@ -126,7 +171,7 @@ struct WaveSlot {
 // decisions, branch-free except the pass re-scan (taken by the wave only when
 // one of its lanes passes).  valid: the action is in possible_moves (`a` in
 // [0, N*N) then).  Returns reward / done / winner (0 unless the game ended).
-template <int N>
+template <int N, int RAYS = RAYS_LDS>
 __device__ __forceinline__ void step1(uint64_t& B, uint64_t& Wt, uint64_t& L, uint32_t& m, int a, bool valid,
                                       uint32_t flags, const uint64_t* __restrict__ rays, int& reward, int& done,
                                       int& winner) {
@@ -135,7 +180,7 @@ __device__ __forceinline__ void step1(uint64_t& B, uint64_t& Wt, uint64_t& L, ui
     const bool tw = (m & M_TURN_WHITE) != 0;
     uint64_t P = tw ? Wt : B, O = tw ? B : Wt;
     const uint64_t mv = valid ? 1ull << a : 0ull;                          // update_board (:391-410)
-    const uint64_t f = flips_rays<N>(P, O, rays + (a & 63)) & (0ull - (uint64_t)valid);
+    const uint64_t f = flips_rays<N, RAYS>(P, O, rays + (a & 63), a) & (0ull - (uint64_t)valid);
     P |= f | mv;
     O &= ~f;
     const bool full = (P | O) == BD;                                        // :425-426
@@ -166,7 +211,7 @@ __device__ __forceinline__ void step1(uint64_t& B, uint64_t& Wt, uint64_t& L, ui
 // One ply of every board, one lane per board.  A grid-stride loop with the
 // next group's loads issued before the current group's work measured slower
 // (1,048,576 boards: 15.4 -> 16.2 us per ply).
-template <int N, int SRC>
+template <int N, int SRC, int RAYS>
 __device__ __forceinline__ void ply_body(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
                                          uint64_t* __restrict__ legal, int E, uint32_t flags,
                                          int32_t* __restrict__ actions, int32_t* __restrict__ rewards,
@@ -175,7 +220,7 @@ __device__ __forceinline__ void ply_body(uint64_t* __restrict__ boards, uint16_t
     static_assert(Geo<N>::W == 1, "one-word boards");
     static_assert(BLOCK * 2 == 8 * 64, "one 16-byte piece of the ray table per thread");
     constexpr int NN = N * N;
-    __shared__ __attribute__((aligned(16))) uint64_t rays[8 * 64];
+    __shared__ __attribute__((aligned(16))) uint64_t rays[RAYS == RAYS_LDS ? 8 * 64 : 1];
     ply += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
     const int t = blockIdx.x * BLOCK + threadIdx.x;
     const bool mine = t < E;
@@ -183,15 +228,18 @@ __device__ __forceinline__ void ply_body(uint64_t* __restrict__ boards, uint16_t
     // every load first, none behind a branch: the ray table's piece first of
     // all (the wave then waits only for it before its LDS store), the board's
     // loads (lanes past E load board E - 1 and store nothing), the wave's slot
-    const ulonglong2 rv = reinterpret_cast<const ulonglong2*>(rays_g)[threadIdx.x];
+    ulonglong2 rv;
+    if constexpr (RAYS == RAYS_LDS) rv = reinterpret_cast<const ulonglong2*>(rays_g)[threadIdx.x];
     const ulonglong2 bw = reinterpret_cast<const ulonglong2*>(boards)[e];
     uint64_t L = legal[e];
     uint32_t m = meta[e];
     int a = 0;
     if constexpr (SRC == PLY_ACTIONS) a = actions[e];
     WaveSlot slot(wdl, t, E);
-    reinterpret_cast<ulonglong2*>(rays)[threadIdx.x] = rv;
-    __syncthreads();
+    if constexpr (RAYS == RAYS_LDS) {
+        reinterpret_cast<ulonglong2*>(rays)[threadIdx.x] = rv;
+        __syncthreads();
+    }
     const uint32_t id = rng.id_base + (uint32_t)e;
     uint64_t B = bw.x, Wt = bw.y;
     const bool was_term = (m & M_TERMINATED) != 0;
@@ -208,7 +256,7 @@ __device__ __forceinline__ void ply_body(uint64_t* __restrict__ boards, uint16_t
         valid = (unsigned)a < (unsigned)NN && ((L >> (a & 63)) & 1ull);  // `action not in possible_moves` (:417)
     }
     int r, d, win;
-    step1<N>(B, Wt, L, m, a, valid, flags, rays, r, d, win);
+    step1<N, RAYS>(B, Wt, L, m, a, valid, flags, rays, r, d, win);
     if (was_term) {  // reference: ValueError (othello.py:415-416); batched: a no-op reporting done
         r = 0;       // (the state is not stored back)
         d = 1;
@@ -244,24 +292,24 @@ __device__ __forceinline__ void ply_body(uint64_t* __restrict__ boards, uint16_t
 
 // oth_step on one-word boards (no register bound: 64 VGPRs forced a spill,
 // whose scratch traffic cost 16 B per board)
-template <int N>
+template <int N, int RAYS>
 __global__ __launch_bounds__(BLOCK) void k_ply_step(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
                                                     uint64_t* __restrict__ legal, int E, uint32_t flags,
                                                     const int32_t* __restrict__ actions, int32_t* __restrict__ rewards,
                                                     uint8_t* __restrict__ dones, unsigned long long* __restrict__ wdl,
                                                     const uint64_t* __restrict__ rays, Rng rng, uint64_t ply) {
-    ply_body<N, PLY_ACTIONS>(boards, meta, legal, E, flags, const_cast<int32_t*>(actions), rewards, dones, wdl, rays,
+    ply_body<N, PLY_ACTIONS, RAYS>(boards, meta, legal, E, flags, const_cast<int32_t*>(actions), rewards, dones, wdl, rays,
                              rng, ply);
 }
 
 // oth_step_policy(RANDOM, 1 ply) on one-word boards
-template <int N>
+template <int N, int RAYS>
 __global__ __launch_bounds__(BLOCK) void k_ply_rand(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
                                                     uint64_t* __restrict__ legal, int E, uint32_t flags,
                                                     int32_t* __restrict__ actions, int32_t* __restrict__ rewards,
                                                     uint8_t* __restrict__ dones, unsigned long long* __restrict__ wdl,
                                                     const uint64_t* __restrict__ rays, Rng rng, uint64_t ply) {
-    ply_body<N, PLY_RANDOM>(boards, meta, legal, E, flags, actions, rewards, dones, wdl, rays, rng, ply);
+    ply_body<N, PLY_RANDOM, RAYS>(boards, meta, legal, E, flags, actions, rewards, dones, wdl, rays, rng, ply);
 }
 
 // oth_create: the handle's ray table (fill_rays<N, true>'s layout) in device memory

@@ -600,3 +600,41 @@ def test_greedy_vs_random_split_near_readme(torch_cuda):
     tot = w + d + l
     assert tot > E
     assert abs(100 * w / tot - 61) < 12 and abs(100 * d / tot - 5) < 5 and abs(100 * l / tot - 34) < 12, (w, d, l)
+
+
+@pytest.mark.parametrize("n,E", [(8, 70001), (6, 70001), (5, 1000), (8, 65536)])
+def test_single_ply_kernels_both_ray_sources(torch_cuda, n, E):
+    """The single-ply kernels (ply.hpp) compute their rays up to 65,536 boards
+    and read the handle's LDS-staged table beyond: both equal the oracle for
+    external actions (legal, illegal, out of range; both sudden-death modes)
+    and for one-ply random play, ragged E included."""
+    torch = torch_cuda
+    rng = np.random.RandomState(E + n)
+    for sd in (True, False):
+        env = make_env(torch, E, n, sd=sd, auto=True, seed=9)
+        s = oracle.reset(n, E)
+        for p in range(6):
+            lb = legal_bool(s.legal, n)
+            pick = np.argmax(rng.rand(E, n * n) * lb, axis=1).astype(np.int32)
+            wild = (rng.rand(E) < 0.1) | ~lb.any(axis=1)
+            acts = np.where(wild, rng.randint(-2, n * n + 2, size=E), pick).astype(np.int32)
+            orw, od, _ = oracle.step(s, flags_of(sd, False, True), acts, seed=9, ply=p)
+            _, rew, dn, _ = env.step(torch.from_numpy(acts).cuda(), observe=False)
+            np.testing.assert_array_equal(rew.cpu().numpy(), orw)
+            np.testing.assert_array_equal(dn.cpu().numpy(), od.astype(bool))
+        b, m, lg = get_state_np(env)
+        np.testing.assert_array_equal(b, s.boards)
+        np.testing.assert_array_equal(m, s.meta)
+        np.testing.assert_array_equal(lg, s.legal)
+        # one-ply random launches from this state (ply counter 6)
+        wdl0 = env.counts().cpu().numpy()
+        acts = [env.step_policy("random", n_plies=1) for _ in range(3)]
+        oa, orw, od, owdl = oracle.rollout(s, flags_of(sd, False, True), 0, 3, seed=9, ply0=6)
+        np.testing.assert_array_equal(torch.cat([a[0] for a in acts]).cpu().numpy(), oa)
+        np.testing.assert_array_equal(torch.cat([a[1] for a in acts]).cpu().numpy(), orw)
+        np.testing.assert_array_equal(torch.cat([a[2] for a in acts]).cpu().numpy(), od)
+        b, m, lg = get_state_np(env)
+        np.testing.assert_array_equal(b, s.boards)
+        np.testing.assert_array_equal(m, s.meta)
+        np.testing.assert_array_equal(lg, s.legal)
+        np.testing.assert_array_equal(env.counts().cpu().numpy() - wdl0, owdl)
