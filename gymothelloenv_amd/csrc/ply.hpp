@@ -210,7 +210,9 @@ __device__ __forceinline__ void step1(uint64_t& B, uint64_t& Wt, uint64_t& L, ui
 
 // One ply of every board, one lane per board.  A grid-stride loop with the
 // next group's loads issued before the current group's work measured slower
-// (1,048,576 boards: 15.4 -> 16.2 us per ply).
+// (1,048,576 boards: 15.4 -> 16.2 us per ply), and so did one streaming the
+// next group into LDS by global_load_lds while the current one computes
+// (15.1 -> 16.8 us with 16 waves per CU, 18.5 with 8).
 template <int N, int SRC, int RAYS>
 __device__ __forceinline__ void ply_body(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
                                          uint64_t* __restrict__ legal, int E, uint32_t flags,
