@@ -183,8 +183,7 @@ OTH_HD BB<W> shift(const BB<W>& x) {
 // A one-word board as two dwords.  hipcc splits 64-bit logic into 32-bit halves
 // only after instruction selection, so `(a & b) | c` on uint64_t becomes four
 // VALU ops; on explicit dwords it becomes v_and_or_b32 / gfx950's 3-input
-// v_bitop3_b32 per half.  Constant shifts are one op per half
-// (v_lshlrev_b32 + v_alignbit_b32) instead of a half-rate v_lshlrev_b64.
+// v_bitop3_b32 per half.  Constant shifts stay one v_lshl*_b64 (sh below).
 struct U2 {
     uint32_t lo, hi;
 };
@@ -198,6 +197,22 @@ OTH_HD bool any(U2 a) { return (a.lo | a.hi) != 0u; }
 template <int S>  // S > 0: toward higher squares; S < 0: toward lower squares
 OTH_HD U2 sh(U2 x) {
     static_assert(S > -64 && S < 64, "shift within one word");
+#if defined(__HIP_DEVICE_COMPILE__)
+    // A shift by 1..31 as ONE v_lshl*_b64 (inline asm: the backend splits a 64-bit
+    // shift of a value used as dwords back into v_lshlrev_b32 + v_alignbit_b32).
+    // With one wave per SIMD an independent 64-bit shift issues in ~6.6 cycles,
+    // the dword pair in ~11.5 (profiles/r01/ubench_valu.json): k_play_rand 8x8
+    // 0.769 -> 0.720 us per ply (profiles/r03/sh64).  Constants still fold.
+    if constexpr (S != 0 && S > -32 && S < 32) {
+        const uint64_t v = u64(x);
+        if (!__builtin_constant_p(v)) {
+            uint64_t r;
+            if constexpr (S > 0) asm("v_lshlrev_b64 %0, %2, %1" : "=v"(r) : "v"(v), "n"(S));
+            else asm("v_lshrrev_b64 %0, %2, %1" : "=v"(r) : "v"(v), "n"(-S));
+            return u2(r);
+        }
+    }
+#endif
     if constexpr (S == 0) {
         return x;
     } else if constexpr (S >= 32) {
@@ -209,6 +224,17 @@ OTH_HD U2 sh(U2 x) {
     } else {
         return U2{(x.lo >> -S) | (x.hi << (32 + S)), x.hi >> -S};
     }
+}
+
+// (a & b) | c per dword: one v_and_or_b32 each (spelled out: with 64-bit
+// shifts in the chain the combiner refactors the first step into or + and)
+OTH_HD U2 and_or(U2 a, U2 b, U2 c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (!__builtin_constant_p(u64(a) ^ u64(b) ^ u64(c)))
+        return U2{(uint32_t)__builtin_amdgcn_bitop3_b32(a.lo, b.lo, c.lo, 0xEA),
+                  (uint32_t)__builtin_amdgcn_bitop3_b32(a.hi, b.hi, c.hi, 0xEA)};
+#endif
+    return (a & b) | c;
 }
 
 // plain 64-bit words with U2's interface (OneWord::greedy runs on either)
@@ -847,16 +873,16 @@ struct OneWord {
         U2 p2{0u, 0u};
         if constexpr (STEPS > 1) p2 = p1 & sh<S>(p1);
         U2 x = sh<S>(P) & p1;
-        x = (p1 & sh<S>(x)) | x;
-        if constexpr (STEPS > 1) x = (p2 & sh<2 * S>(x)) | x;
-        if constexpr (STEPS > 2) x = (p2 & sh<2 * S>(x)) | x;
+        x = and_or(p1, sh<S>(x), x);
+        if constexpr (STEPS > 1) x = and_or(p2, sh<2 * S>(x), x);
+        if constexpr (STEPS > 2) x = and_or(p2, sh<2 * S>(x), x);
         tplus = x;
         L = L | sh<S>(x);
         const U2 p2m = sh<-S>(p2);
         x = sh<-S>(P) & p1;
-        x = (p1 & sh<-S>(x)) | x;
-        if constexpr (STEPS > 1) x = (p2m & sh<-2 * S>(x)) | x;
-        if constexpr (STEPS > 2) x = (p2m & sh<-2 * S>(x)) | x;
+        x = and_or(p1, sh<-S>(x), x);
+        if constexpr (STEPS > 1) x = and_or(p2m, sh<-2 * S>(x), x);
+        if constexpr (STEPS > 2) x = and_or(p2m, sh<-2 * S>(x), x);
         tminus = x;
         L = L | sh<-S>(x);
     }

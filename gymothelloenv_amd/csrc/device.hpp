@@ -142,6 +142,61 @@ struct Start {  // _reset_board (othello.py:256-263): W at (c-1,c-1),(c,c); B at
     static constexpr BB<W> WHITE = make((C - 1) * N + (C - 1), C * N + C);
 };
 
+// black's possible_moves on the reset board (_reset_board + get_possible_actions,
+// othello.py:256-263, 313-343), by a compile-time ray walk
+template <int N>
+constexpr uint64_t start_moves() {
+    static_assert(Geo<N>::W == 1, "one-word boards");
+    const uint64_t B = Start<N>::BLACK.w[0], Wt = Start<N>::WHITE.w[0];
+    uint64_t L = 0;
+    for (int a = 0; a < N * N; ++a) {
+        if (((B | Wt) >> a) & 1ull) continue;
+        for (int dr = -1; dr <= 1; ++dr)
+            for (int dc = -1; dc <= 1; ++dc) {
+                if (!dr && !dc) continue;
+                int r = a / N + dr, c = a % N + dc, run = 0;
+                while (r >= 0 && r < N && c >= 0 && c < N && ((Wt >> (r * N + c)) & 1ull)) {
+                    r += dr;
+                    c += dc;
+                    ++run;
+                }
+                if (run > 0 && r >= 0 && r < N && c >= 0 && c < N && ((B >> (r * N + c)) & 1ull)) L |= 1ull << a;
+            }
+    }
+    return L;
+}
+
+// the Fills engine's eight fills on the reset board, black to move (what
+// OneWord::legal stores in t for the start position), by the same ray walk:
+// t[d] = opponent discs from which going along ray direction d (E, S, SE, SW,
+// W, N, NW, NE) through opponent discs -- of the inner columns, except on the
+// vertical axis, as the scan's propagators -- ends on an own disc
+template <int N>
+struct StartFills {
+    uint64_t t[8];
+};
+template <int N>
+constexpr StartFills<N> start_fills() {
+    static_assert(Geo<N>::W == 1, "one-word boards");
+    const uint64_t P = Start<N>::BLACK.w[0], O = Start<N>::WHITE.w[0], IN = Geo<N>::INNER.w[0];
+    constexpr int DR[8] = {0, 1, 1, 1, 0, -1, -1, -1}, DC[8] = {1, 0, 1, -1, -1, 0, -1, 1};
+    StartFills<N> f{};
+    for (int d = 0; d < 8; ++d) {
+        const uint64_t p1 = DC[d] == 0 ? O : (O & IN);
+        f.t[d] = 0;
+        for (int a = 0; a < N * N; ++a) {
+            if (!((p1 >> a) & 1ull)) continue;
+            int r = a / N + DR[d], c = a % N + DC[d];
+            while (r >= 0 && r < N && c >= 0 && c < N && ((p1 >> (r * N + c)) & 1ull)) {
+                r += DR[d];
+                c += DC[d];
+            }
+            if (r >= 0 && r < N && c >= 0 && c < N && ((P >> (r * N + c)) & 1ull)) f.t[d] |= 1ull << a;
+        }
+    }
+    return f;
+}
+
 template <int N>
 struct Lane {
     static constexpr int W = Geo<N>::W;
@@ -1238,10 +1293,11 @@ __device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_
         // auto-reset (othello.py:256-271): black to move from the start position
         M = Start<N>::BLACK.w[0];
         O = Start<N>::WHITE.w[0];
-        BB<1> sb, sw;
-        sb.w[0] = M;
-        sw.w[0] = O;
-        L = eng.legal(sb, sw).w[0];  // constant: folds to the start position's moves and fills
+        constexpr uint64_t START_MOVES = start_moves<N>();  // constant-evaluated
+        constexpr StartFills<N> SF = start_fills<N>();
+        L = START_MOVES;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) eng.t[k] = SF.t[k];
         uint32_t rl = 0;
         if (rng.init_rand > 0)
             rl = (uint32_t)scale_index(philox_x(rng.seed, id, g, RNG_OPENING_AUTO), rng.init_rand / 2 + 1) * 2u;
@@ -1384,9 +1440,9 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
                         eng.prime(s);
                     }
                 }
-                act_p[(size_t)p * E] = a;
-                rew_p[(size_t)p * E] = r;
-                done_p[(size_t)p * E] = (uint8_t)d;
+                actions[(size_t)p * E + e] = a;
+                rewards[(size_t)p * E + e] = r;
+                dones[(size_t)p * E + e] = (uint8_t)d;
             }
         }
         store_lane<N>(s, boards, meta, legal, e);

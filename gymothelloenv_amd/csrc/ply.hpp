@@ -27,30 +27,6 @@ namespace oth_dev {
 
 constexpr int PLY_ACTIONS = 0, PLY_RANDOM = 1;
 
-// black's possible_moves on the reset board (_reset_board + get_possible_actions,
-// othello.py:256-263, 313-343), by a compile-time ray walk
-template <int N>
-constexpr uint64_t start_moves() {
-    static_assert(Geo<N>::W == 1, "one-word boards");
-    const uint64_t B = Start<N>::BLACK.w[0], Wt = Start<N>::WHITE.w[0];
-    uint64_t L = 0;
-    for (int a = 0; a < N * N; ++a) {
-        if (((B | Wt) >> a) & 1ull) continue;
-        for (int dr = -1; dr <= 1; ++dr)
-            for (int dc = -1; dc <= 1; ++dc) {
-                if (!dr && !dc) continue;
-                int r = a / N + dr, c = a % N + dc, run = 0;
-                while (r >= 0 && r < N && c >= 0 && c < N && ((Wt >> (r * N + c)) & 1ull)) {
-                    r += dr;
-                    c += dc;
-                    ++run;
-                }
-                if (run > 0 && r >= 0 && r < N && c >= 0 && c < N && ((B >> (r * N + c)) & 1ull)) L |= 1ull << a;
-            }
-    }
-    return L;
-}
-
 // Where the flips' rays come from (a template parameter of the single-ply kernels):
 //   RAYS_LDS   the handle's table staged in LDS (fewest VALU: faster where the
 //              launch is bandwidth-bound, 1,048,576 boards 15.8 -> 14.9 us per ply)
