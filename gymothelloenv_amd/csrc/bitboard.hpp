@@ -281,6 +281,16 @@ OTH_HD uint64_t and3_64(uint64_t a, uint64_t b, uint64_t c) {
     return a & b & c;
 #endif
 }
+// a & ~b & c (the lowest set bit of y restricted to c, as (y, y - 1, c)): one 3-input op per dword
+OTH_HD uint64_t andn_and_64(uint64_t a, uint64_t b, uint64_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, 0x20);
+    const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), 0x20);
+    return ((uint64_t)hi << 32) | lo;
+#else
+    return a & ~b & c;
+#endif
+}
 OTH_HD uint64_t maj3_64(uint64_t a, uint64_t b, uint64_t c) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, 0xE8);
@@ -1046,6 +1056,36 @@ OTH_HD int select64(uint64_t x, int k) {
     const int bit = (int)((t >> (2 * (4 * (nib & 7u) + kn))) & 3u);
     return (up ? 32 : 0) + 8 * b + (un ? 4 : 0) + bit;
 }
+// The same select with the bit inside the byte read from a table (sel8: the
+// set-bit positions of every byte value, ascending, one byte each -- 2 KiB in
+// LDS, sel8_word): one ds_read_u8 in place of the nibble step's ~18 VALU.
+OTH_HD constexpr uint64_t sel8_word(uint32_t v) {
+    uint64_t w = 0;
+    int j = 0;
+    for (int b = 0; b < 8; ++b)
+        if ((v >> b) & 1u) {
+            w |= (uint64_t)b << (8 * j);
+            ++j;
+        }
+    return w;
+}
+OTH_HD int select64_tab(uint64_t x, int k, const uint8_t* sel8) {
+    const uint32_t lo = (uint32_t)x;
+    const int c = popc64(lo);
+    const bool up = k >= c;
+    const uint32_t v = up ? (uint32_t)(x >> 32) : lo;
+    const int kk = up ? k - c : k;
+    const int q1 = popc64(v & 0xFFu), q2 = popc64(v & 0xFFFFu), q3 = popc64(v & 0xFFFFFFu);
+    const bool m1 = q1 <= kk, m2 = q2 <= kk, m3 = q3 <= kk;
+    const int b = (int)m1 + (int)m2 + (int)m3;
+    const int qb = m3 ? q3 : (m2 ? q2 : (m1 ? q1 : 0));
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t byte = __builtin_amdgcn_ubfe(v, 8u * (uint32_t)b, 8u);  // v_bfe_u32
+#else
+    const uint32_t byte = (v >> (8 * b)) & 0xFFu;
+#endif
+    return (up ? 32 : 0) + 8 * b + sel8[8 * byte + (uint32_t)(kk - qb)];
+}
 #else
 OTH_HD int select64(uint64_t x, int k) {
     int pos = 0;
@@ -1099,24 +1139,46 @@ OTH_HD int select_bit(const BB<W>& b, int k) {
 struct U4 {
     uint32_t x, y, z, w;
 };
+#ifndef OTH_PHILOX_XOR3
+#define OTH_PHILOX_XOR3 1  // Philox rounds >= 2: each a ^ b ^ k as one v_bitop3_b32 (the backend emits two v_xor_b32)
+#endif
+// a ^ b ^ c; round r of philox4 takes the 3-input form only from round 2 on,
+// where every operand but the key varies per lane (rounds 0 and 1 keep their
+// uniform parts on the scalar unit)
+template <int R>
+OTH_HD uint32_t philox_xor(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (OTH_PHILOX_XOR3 && R >= 2) return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#endif
+    return a ^ b ^ c;
+}
+template <int R>
+OTH_HD void philox_round(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t k0, uint32_t k1) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = philox_xor<R>((uint32_t)(p1 >> 32), c1, k0);
+    const uint32_t n1 = (uint32_t)p1;
+    const uint32_t n2 = philox_xor<R>((uint32_t)(p0 >> 32), c3, k1);
+    const uint32_t n3 = (uint32_t)p0;
+    c0 = n0;
+    c1 = n1;
+    c2 = n2;
+    c3 = n3;
+}
 OTH_HD U4 philox4(uint64_t seed, uint32_t id, uint64_t ctr, uint32_t purpose) {
     uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
     uint32_t c0 = id, c1 = (uint32_t)ctr, c2 = (uint32_t)(ctr >> 32), c3 = purpose;
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
-        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
-        uint32_t n1 = (uint32_t)p1;
-        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
-        uint32_t n3 = (uint32_t)p0;
-        c0 = n0;
-        c1 = n1;
-        c2 = n2;
-        c3 = n3;
-        k0 += 0x9E3779B9u;
-        k1 += 0xBB67AE85u;
-    }
+    constexpr uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+    philox_round<0>(c0, c1, c2, c3, k0, k1);
+    philox_round<1>(c0, c1, c2, c3, k0 + W0, k1 + W1);
+    philox_round<2>(c0, c1, c2, c3, k0 + 2 * W0, k1 + 2 * W1);
+    philox_round<3>(c0, c1, c2, c3, k0 + 3 * W0, k1 + 3 * W1);
+    philox_round<4>(c0, c1, c2, c3, k0 + 4 * W0, k1 + 4 * W1);
+    philox_round<5>(c0, c1, c2, c3, k0 + 5 * W0, k1 + 5 * W1);
+    philox_round<6>(c0, c1, c2, c3, k0 + 6 * W0, k1 + 6 * W1);
+    philox_round<7>(c0, c1, c2, c3, k0 + 7 * W0, k1 + 7 * W1);
+    philox_round<8>(c0, c1, c2, c3, k0 + 8 * W0, k1 + 8 * W1);
+    philox_round<9>(c0, c1, c2, c3, k0 + 9 * W0, k1 + 9 * W1);
     return U4{c0, c1, c2, c3};
 }
 OTH_HD uint32_t philox_x(uint64_t seed, uint32_t id, uint64_t ply, uint32_t purpose) {
@@ -1130,6 +1192,12 @@ OTH_HD uint32_t action_draw(uint64_t seed, uint32_t id, uint64_t g) {
 }
 
 // floor(u * n / 2^32): uniform index in [0, n) (RandomPolicy, simple_policies.py:39).
-OTH_HD int scale_index(uint32_t u, int n) { return (int)(((uint64_t)u * (uint64_t)n) >> 32); }
+OTH_HD int scale_index(uint32_t u, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (int)__umulhi(u, (uint32_t)n);  // a 32-bit result: the callers' compares stay 32-bit
+#else
+    return (int)(((uint64_t)u * (uint64_t)n) >> 32);
+#endif
+}
 
 }  // namespace oth

@@ -1237,6 +1237,19 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
 struct NoFill {
     __device__ __forceinline__ void operator()() const {}
 };
+#ifndef OTH_SELECT_LDS
+#define OTH_SELECT_LDS 1  // k_play_rand: the bit inside the byte of the k-th legal square from a 2-KiB LDS table
+#endif
+#ifndef OTH_TALLY_SIGN
+#define OTH_TALLY_SIGN 1  // play_rand_fast tallies (sum of black's signs, games, decided games)
+#endif
+// black wins / draws / white wins from play_rand_fast's (sum of black's signs, games, decided games)
+__device__ __forceinline__ void tally_from_signs(uint32_t s, uint32_t g, uint32_t z, uint32_t& cb, uint32_t& cd,
+                                                 uint32_t& cw) {
+    cb += (z + s) >> 1;
+    cw += (z - s) >> 1;
+    cd += g - z;
+}
 // FILL: independent work (the next Philox block) run after the opponent's scan
 // and pinned there, so that it shares the ply's first scheduling region with the
 // pick, the ray-table loads, the flips and the scan (OTH_RAND_FILL)
@@ -1244,13 +1257,24 @@ template <int N, int POLICY = OTH_POLICY_RANDOM, bool OPEN = true, typename Eng 
 __device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_t& L, uint32_t& meta,
                                                const Eng& eng, uint32_t u, uint32_t flags, const Rng& rng,
                                                uint32_t id, uint64_t g, int& a, int& r, int& d, uint32_t& cb,
-                                               uint32_t& cd, uint32_t& cw, const FILL& fill = FILL{}) {
+                                               uint32_t& cd, uint32_t& cw, const FILL& fill = FILL{},
+                                               const uint8_t* sel8 = nullptr) {
     constexpr uint64_t BD = Geo<N>::BOARD.w[0];
     constexpr int NN = N * N;
+    // the k-th legal square: the nibble step by arithmetic, or the byte's bit from the LDS table
+    auto pick = [&](uint32_t draw) __attribute__((always_inline)) {
+        const int k = scale_index(draw, popc64(L));
+#if OTH_SELECT_LDS
+        return select64_tab(L, k, sel8);
+#else
+        (void)sel8;
+        return select64(L, k);
+#endif
+    };
     if constexpr (POLICY == OTH_POLICY_RANDOM) {
-        a = select64(L, scale_index(u, popc64(L)));  // RandomPolicy (simple_policies.py:37-41); L != 0
+        a = pick(u);  // RandomPolicy (simple_policies.py:37-41); L != 0
     } else if constexpr (OPEN) {
-        if (meta & 0xff00u) a = select64(L, scale_index(action_draw(rng.seed, id, g), popc64(L)));
+        if (meta & 0xff00u) a = pick(action_draw(rng.seed, id, g));
         else a = OneWord<N>::greedy(eng.t, L);
     } else {
         a = OneWord<N>::greedy(eng.t, L);
@@ -1282,14 +1306,25 @@ __device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_
     r = 0;
     d = term ? 1 : 0;
     if (term) {
+        const int pc = popc64(Mn), oc = popc64(On), df = pc - oc;
+        const int sg = min(max(df, -1), 1);  // v_med3_i32: the mover's result
+        if (flags & OTH_DISK_REWARD) r = oc == 0 ? NN : df;  // :446-459
+        else r = sg;                                           // winner * player_turn
+#if OTH_TALLY_SIGN
+        // the tally as (cb, cd, cw) = (sum of black's signs, games, decided games),
+        // turned into wins / draws / wins by tally_from_signs: three adds, no selects
+        const int m = -(int)(meta & M_TURN_WHITE);  // the mover (the turn is not passed on): 0 black, -1 white
+        const int sb = (sg ^ m) - m;                // black's result
+        cb += (uint32_t)sb;
+        cd += 1u;
+        cw += (uint32_t)__mul24(sb, sb);
+#else
         const bool tw = (meta & M_TURN_WHITE) != 0;  // the side that just moved (the turn is not passed on)
-        const int pc = popc64(Mn), oc = popc64(On);
-        if (flags & OTH_DISK_REWARD) r = oc == 0 ? NN : pc - oc;  // :446-459
-        else r = pc > oc ? 1 : (pc < oc ? -1 : 0);                  // winner * player_turn
         const bool mover_wins = pc > oc, opp_wins = pc < oc;
         cb += tw ? opp_wins : mover_wins;
         cd += !mover_wins && !opp_wins;
         cw += tw ? mover_wins : opp_wins;
+#endif
         // auto-reset (othello.py:256-271): black to move from the start position
         M = Start<N>::BLACK.w[0];
         O = Start<N>::WHITE.w[0];
@@ -1314,7 +1349,14 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
     static_assert(Geo<N>::W == 1, "one-word boards");
     ply0 += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
     __shared__ __attribute__((aligned(16))) uint64_t lds_rays[Fills<N>::RAY_WORDS];
-    fill_rays<N, turned_rays<Fills<N>>::value>(lds_rays);
+#if OTH_SELECT_LDS
+    __shared__ __attribute__((aligned(16))) uint64_t lds_sel[256];
+    for (int i = threadIdx.x; i < 256; i += BLOCK) lds_sel[i] = sel8_word((uint32_t)i);
+    const uint8_t* sel8 = reinterpret_cast<const uint8_t*>(lds_sel);
+#else
+    const uint8_t* sel8 = nullptr;
+#endif
+    fill_rays<N, turned_rays<Fills<N>>::value>(lds_rays);  // (its barrier covers lds_sel)
     const int e = blockIdx.x * BLOCK + threadIdx.x;
     uint32_t cb = 0, cd = 0, cw = 0;
     if (e < E) {
@@ -1338,12 +1380,17 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
         int32_t* act_p = actions + e;
         int32_t* rew_p = rewards + e;
         uint8_t* done_p = dones + e;
+#if OTH_TALLY_SIGN
+        uint32_t t0 = 0, t1 = 0, t2 = 0;  // play_rand_fast's tally (tally_from_signs)
+#else
+        uint32_t &t0 = cb, &t1 = cd, &t2 = cw;
+#endif
         auto fast = [&](auto OPENC) __attribute__((always_inline)) {
         constexpr bool OPEN = decltype(OPENC)::value;
         auto ply = [&](int p, uint32_t u, const auto& fill) __attribute__((always_inline)) {
             int a, r, d;
-            play_rand_fast<N, POLICY, OPEN>(M, O, L, mt, eng, u, flags, rng, id, ply0 + (uint64_t)p, a, r, d, cb, cd,
-                                            cw, fill);
+            play_rand_fast<N, POLICY, OPEN>(M, O, L, mt, eng, u, flags, rng, id, ply0 + (uint64_t)p, a, r, d, t0, t1,
+                                            t2, fill, sel8);
             *act_p = a;
             *rew_p = r;
             *done_p = (uint8_t)d;
@@ -1416,6 +1463,9 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
             // no opening bookkeeping when no board of the wave can have opening plies
             if (OTH_OPEN_SPLIT && rng.init_rand == 0 && !__any((mt & 0xff00u) != 0)) fast(std::false_type{});
             else fast(std::true_type{});
+#if OTH_TALLY_SIGN
+            tally_from_signs(t0, t1, t2, cb, cd, cw);
+#endif
             const bool tw = (mt & M_TURN_WHITE) != 0;
             s.white.w[0] = tw ? M : O;
             s.black.w[0] = tw ? O : M;

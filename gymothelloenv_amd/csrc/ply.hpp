@@ -27,6 +27,10 @@ namespace oth_dev {
 
 constexpr int PLY_ACTIONS = 0, PLY_RANDOM = 1;
 
+#ifndef OTH_CAP_BITOP3
+#define OTH_CAP_BITOP3 1  // capped_run's cap test as one v_bitop3_b32 per dword (the backend rewrites ~(y - 1) as -y: six ops)
+#endif
+
 // Where the flips' rays come from (a template parameter of the single-ply kernels):
 //   RAYS_LDS   the handle's table staged in LDS (fewest VALU: faster where the
 //              launch is bandwidth-bound, 1,048,576 boards 15.8 -> 14.9 us per ply)
@@ -75,7 +79,11 @@ __device__ __forceinline__ uint64_t capped_run(uint64_t ray, uint64_t P, uint64_
     const uint64_t y = ray & ~O;
     const uint64_t ym = y - 1ull;
     const uint64_t run = and3_64(ray, O, ym);
+#if OTH_CAP_BITOP3
+    const uint64_t cap = andn_and_64(y, ym, P);  // y0 if it is an own disc (y & ~(y - 1) & P)
+#else
     const uint64_t cap = y & ~ym & P;  // y0 if it is an own disc
+#endif
     return cap ? run : 0ull;
 }
 

@@ -87,12 +87,15 @@ def test_flips_host_build(hostlib, n):
     np.testing.assert_array_equal(out, opp & ~s.boards[:, :W])
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3])
 def test_select_variants_every_rank(variant):
-    """Both select64 forms (OTH_SELECT=1 binary search, 2 byte-parallel), every
-    rank k of dense and sparse (legal-mask-like) words."""
-    L = build_host(os.path.join(HERE, "host", "libbitboard_host_sel%d.so" % variant), ["-DOTH_SELECT=%d" % variant])
-    L.host_select.argtypes = [ctypes.c_uint64, ctypes.c_int]
+    """Every select form (OTH_SELECT=1 binary search, 2 byte-parallel, 3 = 2 with
+    the bit inside the byte from k_play_rand's sel8 table), every rank k of dense
+    and sparse (legal-mask-like) words."""
+    L = build_host(os.path.join(HERE, "host", "libbitboard_host_sel%d.so" % min(variant, 2)),
+                   ["-DOTH_SELECT=%d" % min(variant, 2)])
+    sel = L.host_select_tab if variant == 3 else L.host_select
+    sel.argtypes = [ctypes.c_uint64, ctypes.c_int]
     rng = np.random.RandomState(variant)
     words = [1, 1 << 63, (1 << 64) - 1, 0x8000000000000001, 0x0101010101010101, 0xF0]
     for _ in range(1500):
@@ -105,7 +108,7 @@ def test_select_variants_every_rank(variant):
     for x in words:
         bits = [i for i in range(64) if (x >> i) & 1]
         for k, b in enumerate(bits):
-            assert L.host_select(x, k) == b, (hex(x), k)
+            assert sel(x, k) == b, (hex(x), k)
 
 
 RAY_DIRS = [(0, 1), (1, 0), (1, 1), (1, -1), (0, -1), (-1, 0), (-1, -1), (-1, 1)]  # E S SE SW W N NW NE
