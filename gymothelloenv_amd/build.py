@@ -71,9 +71,13 @@ def _jobs():
     return max(1, min(n, cap, len(SIZES) + 2))
 
 
-def build(force=False, verbose=True, extra_flags=(), out=OUT, jobs=None):
+def build(force=False, verbose=True, extra_flags=(), out=OUT, jobs=None, only_sizes=None):
+    """only_sizes (A/B variants of the tools, never the shipped library): compile the
+    per-N units of these board sizes only and link the other sizes' objects of the
+    main build (which must exist) -- a variant of one size in a fraction of the time."""
     if not force and not needs_build(out, extra_flags):
         return out
+    assert only_sizes is None or out != OUT, "the shipped library is always built whole"
     digest = source_hash(extra_flags)
     objdir = OBJDIR if out == OUT else os.path.join(OBJDIR, os.path.splitext(os.path.basename(out))[0])
     shutil.rmtree(objdir, ignore_errors=True)
@@ -96,8 +100,17 @@ def build(force=False, verbose=True, extra_flags=(), out=OUT, jobs=None):
 
     if verbose:
         print("hipcc %s -> %s (%d units, src %s)" % (" ".join(base[1:]), out, len(units), digest[:16]), flush=True)
+    reuse = []
+    if only_sizes is not None:
+        keep = {"capi.o", "masked.o"} | {"kernels_n%d.o" % n for n in only_sizes} | {"play_rand_n%d.o" % n
+                                                                                   for n in only_sizes}
+        reuse = [os.path.join(OBJDIR, os.path.basename(u[1])) for u in units if os.path.basename(u[1]) not in keep]
+        units = [u for u in units if os.path.basename(u[1]) in keep]
+        missing = [o for o in reuse if not os.path.exists(o)]
+        if missing:
+            raise RuntimeError("only_sizes needs the main build's objects: %s" % missing[:3])
     with concurrent.futures.ThreadPoolExecutor(jobs or _jobs()) as ex:
-        objs = list(ex.map(compile_one, units))
+        objs = list(ex.map(compile_one, units)) + reuse
     subprocess.check_call([HIPCC, "--offload-arch=%s" % ARCH, "-shared", "-o", out + ".tmp"] + objs, cwd=ROOT)
     os.replace(out + ".tmp", out)
     return out

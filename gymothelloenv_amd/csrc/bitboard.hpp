@@ -1113,6 +1113,24 @@ OTH_HD int select64(uint64_t x, int k) {
 }
 #endif
 
+#if OTH_SELECT == 2
+// select_bit with select64_tab inside the word (k < popcount: a pick from a non-empty mask)
+template <int W>
+OTH_HD int select_bit_tab(const BB<W>& b, int k, const uint8_t* sel8) {
+    int res = 0;
+    bool found = false;
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+        const int c = popc64(b.w[i]);
+        if (!found && k < c) {
+            res = 64 * i + select64_tab(b.w[i], k, sel8);
+            found = true;
+        }
+        if (!found) k -= c;
+    }
+    return res;
+}
+#endif
 template <int W>
 OTH_HD int select_bit(const BB<W>& b, int k) {
     if constexpr (W == 1) {  // branch-free: -1 when k >= popcount (no legal move)

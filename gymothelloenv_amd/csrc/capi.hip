@@ -152,7 +152,9 @@ int oth_create(int32_t n_envs, int32_t board_size, uint32_t flags, uint64_t seed
     hipError_t err = hipMalloc((void**)&env->boards, E * 2 * W * sizeof(uint64_t));
     if (err == hipSuccess) err = hipMalloc((void**)&env->meta, ((E * sizeof(uint16_t) + 15) / 16) * 16);
     if (err == hipSuccess) err = hipMalloc((void**)&env->legal, E * W * sizeof(uint64_t));
-    env->nslots = (int32_t)((4 * (int64_t)E + BLOCK - 1) / BLOCK);  // the widest grid (k_sample_step4: 4 lanes per board)
+    // one W/D/L slot per wave of the widest single-ply grid (k_sample_step4: 4 lanes per board) -- also
+    // more than the per-block slots of every multi-ply launch
+    env->nslots = (int32_t)((4 * (int64_t)E + 63) / 64);
     const size_t slot_bytes = (size_t)env->nslots * 4 * sizeof(unsigned long long);
     if (err == hipSuccess) err = hipMalloc((void**)&env->wdl, slot_bytes);
     if (err == hipSuccess) err = hipMemset(env->wdl, 0, slot_bytes);

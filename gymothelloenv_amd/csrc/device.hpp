@@ -1,5 +1,5 @@
 // device.hpp -- HIP/CDNA4 device code of the vectorised Othello rules engine:
-// per-lane board state, the rule engines (Solo / Rays / Duo), policies and
+// per-lane board state, the rule engines (Solo / Rays / Fills / Quartet), policies and
 // every __global__ kernel template.  Included by kernels_n.hip (compiled once
 // per board size N, so the templates build in parallel) and by capi.hip.
 //
@@ -252,10 +252,8 @@ __device__ __forceinline__ void store_lane(const Lane<N>& s, uint64_t* __restric
 // Engines: who computes legal moves and flips for a lane.
 //   Solo<N>: one lane per board, all 8 directions (any N).
 //   Rays<N>: Solo with LDS ray-table flips (N <= 8).
-//   Duo<N>:  two lanes per board (N <= 8): each lane of the pair scans half
-//            the directions and the halves are or-ed through a DPP quad_perm
-//            swap.  Twice the waves for the same boards, so two waves share
-//            each SIMD's issue slots instead of one wave issuing alone.
+//   Quartet<N>: four lanes per board (N <= 8): each lane of the quad scans
+//            one axis and the parts are or-ed through DPP quad_perm steps.
 // ---------------------------------------------------------------------------
 template <int N>
 struct Solo {
@@ -526,94 +524,14 @@ struct is_fills_w : std::false_type {};
 template <int N>
 struct is_fills_w<FillsW<N>> : std::true_type {};
 
-// the other lane of the pair (lanes 2k, 2k+1): DPP quad_perm [1,0,3,2]
-__device__ __forceinline__ uint32_t pair_swap32(uint32_t x) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
-}
-__device__ __forceinline__ uint64_t pair_swap(uint64_t x) {
-    return ((uint64_t)pair_swap32((uint32_t)(x >> 32)) << 32) | pair_swap32((uint32_t)x);
-}
-
-// Duo<N>: two lanes per board (N <= 8, one word); each lane runs the Solo/Rays
-// algorithms on half the geometry: lane 0 the E/W and S/N axes, lane 1 the two
-// diagonal axes (legal_axis with per-lane shift amounts), and the ray-table
-// flips of its four directions.  Every decision of step_lane is taken on the
-// or-ed (pair-uniform) masks, so both lanes of a pair always follow the same
-// branches and the DPP swap never reads an inactive lane.
-template <int N>
-struct Duo {
-    static_assert(Geo<N>::W == 1, "Duo engine is for one-word boards (N <= 8)");
-    static constexpr int LANES = 2;
-    static constexpr int RAY_WORDS = 8 * 64;
-    static constexpr int STEPS = Pro<N, 0, 1>::STEPS;
-    static constexpr uint64_t BD = Geo<N>::BOARD.w[0], IN = Geo<N>::INNER.w[0];
-    const uint64_t* rays;  // this lane's first "up" table (E or SE)
-    uint32_t sA, sB;       // axis shifts: lane 0 {1, N}, lane 1 {N+1, N-1}
-    uint64_t mB;           // propagator mask of axis B: the vertical axis may pass edge columns
-    int h;
-    __device__ __forceinline__ Duo(int lane_half, const uint64_t* lds) : h(lane_half) {
-        rays = lds + 128 * lane_half;
-        sA = lane_half ? N + 1 : 1;
-        sB = lane_half ? N - 1 : N;
-        mB = lane_half ? IN : BD;
-    }
-    __device__ __forceinline__ static void axis(uint64_t P, uint64_t p1, uint32_t s, uint64_t& L) {
-        uint64_t p2 = 0, p4 = 0;
-        if constexpr (STEPS > 1) p2 = p1 & (p1 << s);
-        if constexpr (STEPS > 2) p4 = p2 & (p2 << (2 * s));
-        uint64_t t = (P << s) & p1;
-        t |= p1 & (t << s);
-        if constexpr (STEPS > 1) t |= p2 & (t << (2 * s));
-        if constexpr (STEPS > 2) t |= p4 & (t << (4 * s));
-        L |= t << s;
-        t = (P >> s) & p1;
-        t |= p1 & (t >> s);
-        if constexpr (STEPS > 1) t |= (p2 >> s) & (t >> (2 * s));
-        if constexpr (STEPS > 2) t |= (p4 >> (3 * s)) & (t >> (4 * s));
-        L |= t >> s;
-    }
-    __device__ __forceinline__ BB<1> legal(const BB<1>& Pb, const BB<1>& Ob) const {
-        const uint64_t P = Pb.w[0], O = Ob.w[0];
-        uint64_t L = 0;
-        axis(P, O & IN, sA, L);
-        axis(P, O & mB, sB, L);
-        L |= pair_swap(L);
-        BB<1> r;
-        r.w[0] = L & ~(P | O) & BD;
-        return r;
-    }
-    __device__ __forceinline__ BB<1> flip(const BB<1>& Pb, const BB<1>& Ob, int a) const {
-        const uint64_t P = Pb.w[0], nO = ~Ob.w[0];
-        const uint64_t* r = rays + a;
-        uint64_t f = 0;
-#pragma unroll
-        for (int d = 0; d < 2; ++d) {  // toward higher squares: E, S | SE, SW
-            const uint64_t ray = r[64 * d];
-            const uint64_t x = ray & nO;
-            const uint64_t fb = x & (0ull - x);
-            f |= (fb & P) ? (ray & (fb - 1ull)) : 0ull;
-        }
-#pragma unroll
-        for (int d = 4; d < 6; ++d) {  // toward lower squares: W, N | NW, NE
-            const uint64_t ray = r[64 * d];
-            const uint64_t x = ray & nO;
-            const uint64_t hb = x ? (0x8000000000000000ull >> __clzll(x)) : 0ull;
-            f |= (hb & P) ? (ray & (0ull - (hb << 1))) : 0ull;
-        }
-        f |= pair_swap(f);
-        BB<1> out;
-        out.w[0] = f;
-        return out;
-    }
-    __device__ __forceinline__ void prime(const Lane<N>&) const {}
-    __device__ __forceinline__ bool leader() const { return h == 0; }
-};
 
 // Quartet<N>: four lanes per board (N <= 8, one word), lanes 4k..4k+3 of a DPP
 // quad: lane q scans one axis (E/W, S/N, SE/NW, SW/NE) and computes the flips
 // of its two ray directions (q toward higher squares, q + 4 toward lower);
-// the four parts are or-ed through quad_perm [1,0,3,2] and [2,3,0,1].  As in
-// Duo, every decision of step_lane is taken on quad-uniform values.
+// the four parts are or-ed through quad_perm [1,0,3,2] and [2,3,0,1].  Every
+// decision of step_lane is taken on the or-ed (quad-uniform) masks, so the four
+// lanes always follow the same branches and the DPP steps never read an
+// inactive lane.
 template <int N>
 struct Quartet {
     static_assert(Geo<N>::W == 1, "Quartet engine is for one-word boards (N <= 8)");
@@ -629,6 +547,23 @@ struct Quartet {
         sh = lane_q == 0 ? 1u : (lane_q == 1 ? (uint32_t)N : (lane_q == 2 ? N + 1u : N - 1u));
         pm = lane_q == 1 ? BD : IN;
     }
+    static constexpr int STEPS = Pro<N, 0, 1>::STEPS;
+    // legal_moves along one axis (+s and -s) with a per-lane shift amount
+    __device__ __forceinline__ static void axis(uint64_t P, uint64_t p1, uint32_t s, uint64_t& L) {
+        uint64_t p2 = 0, p4 = 0;
+        if constexpr (STEPS > 1) p2 = p1 & (p1 << s);
+        if constexpr (STEPS > 2) p4 = p2 & (p2 << (2 * s));
+        uint64_t t = (P << s) & p1;
+        t |= p1 & (t << s);
+        if constexpr (STEPS > 1) t |= p2 & (t << (2 * s));
+        if constexpr (STEPS > 2) t |= p4 & (t << (4 * s));
+        L |= t << s;
+        t = (P >> s) & p1;
+        t |= p1 & (t >> s);
+        if constexpr (STEPS > 1) t |= (p2 >> s) & (t >> (2 * s));
+        if constexpr (STEPS > 2) t |= (p4 >> (3 * s)) & (t >> (4 * s));
+        L |= t >> s;
+    }
     __device__ __forceinline__ static uint32_t quad_or32(uint32_t x) {
         x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
         return x | (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);
@@ -639,7 +574,7 @@ struct Quartet {
     __device__ __forceinline__ BB<1> legal(const BB<1>& Pb, const BB<1>& Ob) const {
         const uint64_t P = Pb.w[0], O = Ob.w[0];
         uint64_t L = 0;
-        Duo<N>::axis(P, O & pm, sh, L);
+        axis(P, O & pm, sh, L);
         BB<1> r;
         r.w[0] = quad_or(L) & ~(P | O) & BD;
         return r;
@@ -1083,6 +1018,46 @@ __global__ __launch_bounds__(BLOCK) void k_reset(uint64_t* __restrict__ boards, 
 }
 
 // oth_step: external actions, one ply.
+// Per-wave W/D/L slot of a single-ply launch: slot w of the handle's
+// [nslots][4] array belongs to wave w of the grid (nslots = ceil(4E / 64) covers
+// every wave of a grid of up to four lanes per board; a wave past E reads the
+// last live wave's slot and never writes).  The wave's counts accumulate in SGPRs over its boards (three
+// ballots per group of 64) and lane 0 adds them with plain stores at the end.
+// Launches on a stream are ordered, so the read at a launch's start sees every
+// earlier launch's adds.
+struct WaveSlot {
+    unsigned long long* p;
+    unsigned long long v0, v1, v2;
+    uint32_t nb = 0, nd = 0, nw = 0;
+    __device__ __forceinline__ WaveSlot(unsigned long long* wdl, int t, int E) : WaveSlot(wdl, min(t >> 6, (E - 1) >> 6)) {}
+    // slot `wave` (the caller's wave index, clamped to its last live wave)
+    __device__ __forceinline__ explicit WaveSlot(unsigned long long* wdl, int wave) {
+        // wave-uniform: the slot is read by scalar loads into SGPRs (the values
+        // live through the whole kernel; written back by lane 0's vector stores)
+        const int w = __builtin_amdgcn_readfirstlane(wave);
+        p = wdl + 4 * (size_t)w;
+        const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(p);
+        v0 = a.x;
+        v1 = a.y;
+        v2 = p[2];
+    }
+    // {black wins, draws, white wins} of this wave's lanes (0 / 1 each)
+    __device__ __forceinline__ void count(bool b, bool d, bool w) {
+        nb += (uint32_t)__popcll(__ballot(b));
+        nd += (uint32_t)__popcll(__ballot(d));
+        nw += (uint32_t)__popcll(__ballot(w));
+    }
+    __device__ __forceinline__ void flush() const {
+        if ((nb | nd | nw) && (threadIdx.x & 63) == 0) {
+            ulonglong2 a;
+            a.x = v0 + nb;
+            a.y = v1 + nd;
+            *reinterpret_cast<ulonglong2*>(p) = a;
+            p[2] = v2 + nw;
+        }
+    }
+};
+
 template <int N>
 __global__ __launch_bounds__(BLOCK) void k_step(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
                                                 uint64_t* __restrict__ legal, int E, uint32_t flags,
@@ -1092,6 +1067,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(uint64_t* __restrict__ boards, u
     ply += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
     const int e = blockIdx.x * BLOCK + threadIdx.x;
     uint32_t cb = 0, cd = 0, cw = 0;
+    WaveSlot slot(wdl, e, E);
     if (e < E) {
         Lane<N> s;
         load_lane<N>(s, boards, meta, legal, e);
@@ -1110,12 +1086,13 @@ __global__ __launch_bounds__(BLOCK) void k_step(uint64_t* __restrict__ boards, u
         if (rewards) rewards[e] = r;
         if (dones) dones[e] = (uint8_t)d;
     }
-    tally(wdl, cb, cd, cw);
+    slot.count(cb != 0, cd != 0, cw != 0);
+    slot.flush();
 }
 
 // oth_step_policy: `plies` plies of on-device play with the board kept in
 // registers between plies; per-ply outputs stored [ply][E].  Eng::LANES lanes
-// per board (Solo/Rays: 1, Duo: 2); only the pair's leader lane stores.
+// per board (Eng::LANES); only the group's leader lane stores.
 // REC: all three per-ply outputs requested (stores without per-pointer branches,
 // so the ply's tail stays one basic block the scheduler can interleave).
 template <int N, int POLICY, typename Eng, bool REC>
@@ -1507,10 +1484,15 @@ template <int N>
 __device__ __forceinline__ void play_rand_fast_w(BB<Geo<N>::W>& M, BB<Geo<N>::W>& O, BB<Geo<N>::W>& L,
                                                  uint32_t& meta, const FillsW<N>& eng, uint32_t u, uint32_t flags,
                                                  const Rng& rng, uint32_t id, uint64_t g, int& a, int& r, int& d,
-                                                 uint32_t& cb, uint32_t& cd, uint32_t& cw) {
+                                                 uint32_t& cb, uint32_t& cd, uint32_t& cw, const uint8_t* sel8) {
     constexpr int W = Geo<N>::W;
     constexpr int NN = N * N;
+#if OTH_SELECT_LDS
+    a = select_bit_tab(L, scale_index(u, popcount(L)), sel8);  // RandomPolicy (simple_policies.py:37-41); L != 0
+#else
+    (void)sel8;
     a = select_bit(L, scale_index(u, popcount(L)));  // RandomPolicy (simple_policies.py:37-41); L != 0
+#endif
     meta -= (meta & 0xff00u) ? (1u << M_RAND_SHIFT) : 0u;
     const BB<W> m = square<W>(a);
     const BB<W> f = eng.flip(M, O, a);  // update_board (othello.py:391-410)
@@ -1531,14 +1513,23 @@ __device__ __forceinline__ void play_rand_fast_w(BB<Geo<N>::W>& M, BB<Geo<N>::W>
     r = 0;
     d = term ? 1 : 0;
     if (term) {
+        const int pc = popcount(Mn), oc = popcount(On), df = pc - oc;
+        const int sg = min(max(df, -1), 1);  // the mover's result
+        if (flags & OTH_DISK_REWARD) r = oc == 0 ? NN : df;  // :446-459
+        else r = sg;
+#if OTH_TALLY_SIGN
+        const int mw = -(int)(meta & M_TURN_WHITE);  // (cb, cd, cw) as in play_rand_fast
+        const int sb = (sg ^ mw) - mw;
+        cb += (uint32_t)sb;
+        cd += 1u;
+        cw += (uint32_t)__mul24(sb, sb);
+#else
         const bool tw = (meta & M_TURN_WHITE) != 0;
-        const int pc = popcount(Mn), oc = popcount(On);
-        if (flags & OTH_DISK_REWARD) r = oc == 0 ? NN : pc - oc;  // :446-459
-        else r = pc > oc ? 1 : (pc < oc ? -1 : 0);
         const bool mover_wins = pc > oc, opp_wins = pc < oc;
         cb += tw ? opp_wins : mover_wins;
         cd += !mover_wins && !opp_wins;
         cw += tw ? mover_wins : opp_wins;
+#endif
         M = Start<N>::BLACK;  // auto-reset (othello.py:256-271)
         O = Start<N>::WHITE;
         L = eng.legal(M, O);
@@ -1560,7 +1551,14 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand_w(uint64_t* __restrict__ bo
     static_assert(W > 1, "multi-word boards");
     ply0 += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
     __shared__ __attribute__((aligned(16))) uint64_t lds_rays[FillsW<N>::RAY_WORDS];
-    FillsW<N>::fill(lds_rays);
+#if OTH_SELECT_LDS
+    __shared__ __attribute__((aligned(16))) uint64_t lds_sel[256];
+    for (int i = threadIdx.x; i < 256; i += BLOCK) lds_sel[i] = sel8_word((uint32_t)i);
+    const uint8_t* sel8 = reinterpret_cast<const uint8_t*>(lds_sel);
+#else
+    const uint8_t* sel8 = nullptr;
+#endif
+    FillsW<N>::fill(lds_rays);  // (its barrier covers lds_sel)
     const int e = blockIdx.x * BLOCK + threadIdx.x;
     uint32_t cb = 0, cd = 0, cw = 0;
     if (e < E) {
@@ -1581,9 +1579,14 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand_w(uint64_t* __restrict__ bo
         int32_t* act_p = actions + e;
         int32_t* rew_p = rewards + e;
         uint8_t* done_p = dones + e;
+#if OTH_TALLY_SIGN
+        uint32_t t0 = 0, t1 = 0, t2 = 0;  // play_rand_fast_w's tally (tally_from_signs)
+#else
+        uint32_t &t0 = cb, &t1 = cd, &t2 = cw;
+#endif
         auto ply = [&](uint64_t g, uint32_t u) __attribute__((always_inline)) {
             int a, r, d;
-            play_rand_fast_w<N>(M, O, L, mt, eng, u, flags, rng, id, g, a, r, d, cb, cd, cw);
+            play_rand_fast_w<N>(M, O, L, mt, eng, u, flags, rng, id, g, a, r, d, t0, t1, t2, sel8);
             *act_p = a;
             *rew_p = r;
             *done_p = (uint8_t)d;
@@ -1607,6 +1610,9 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand_w(uint64_t* __restrict__ bo
                     ++p;
                 }
             }
+#if OTH_TALLY_SIGN
+            tally_from_signs(t0, t1, t2, cb, cd, cw);
+#endif
             const bool tw = (mt & M_TURN_WHITE) != 0;
 #pragma unroll
             for (int i = 0; i < W; ++i) {

@@ -70,9 +70,9 @@ int launch_step(oth_env* env, const int32_t* actions, int32_t* rewards, uint8_t*
                                env->meta, env->legal, env->E, env->flags, actions, rewards, dones, env->wdl, env->rays,
                                rng_of(env), ply);
         else
-            hipLaunchKernelGGL((k_ply_step<N, RAYS_LDS>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards,
-                               env->meta, env->legal, env->E, env->flags, actions, rewards, dones, env->wdl, env->rays,
-                               rng_of(env), ply);
+            hipLaunchKernelGGL((k_ply_step<N, OTH_PLY_BIG_RAYS>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st,
+                               env->boards, env->meta, env->legal, env->E, env->flags, actions, rewards, dones,
+                               env->wdl, env->rays, rng_of(env), ply);
         return after_launch("oth_step");
     }
     hipLaunchKernelGGL(k_step<N>, dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards, env->meta, env->legal,
@@ -93,9 +93,9 @@ void launch_k_play(int lanes_per_board, oth_env* env, int policy, int n_plies, i
                                    env->meta, env->legal, env->E, env->flags, actions, rewards, dones, env->wdl,
                                    env->rays, rng_of(env), ply0);
             else
-                hipLaunchKernelGGL((k_ply_rand<N, RAYS_LDS>), dim3(grid_for(env->E)), block, 0, st, env->boards,
-                                   env->meta, env->legal, env->E, env->flags, actions, rewards, dones, env->wdl,
-                                   env->rays, rng_of(env), ply0);
+                hipLaunchKernelGGL((k_ply_rand<N, OTH_PLY_BIG_RAYS>), dim3(grid_for(env->E)), block, 0, st,
+                                   env->boards, env->meta, env->legal, env->E, env->flags, actions, rewards, dones,
+                                   env->wdl, env->rays, rng_of(env), ply0);
             return;
         }
     }

@@ -37,7 +37,13 @@ constexpr int PLY_ACTIONS = 0, PLY_RANDOM = 1;
 //   RAYS_MATH  computed per move, no table, no LDS, no barrier (+32 VALU: faster
 //              where one wave per SIMD runs a latency-bound chain, 65,536
 //              boards 3.37 -> 3.11 us per ply; profiles/r03/ab/ab_blocks.jsonl)
-constexpr int RAYS_LDS = 1, RAYS_MATH = 2;
+//   RAYS_HALF  the table's four up directions staged in LDS (8 bytes per thread,
+//              half the table traffic); a turned down ray of square a is the up
+//              ray of square NN-1-a (RayMath below)
+constexpr int RAYS_LDS = 1, RAYS_MATH = 2, RAYS_HALF = 3;
+#ifndef OTH_PLY_BIG_RAYS
+#define OTH_PLY_BIG_RAYS RAYS_LDS  // the ray source of single-ply launches above OTH_PLY_MATH_MAX_E boards
+#endif
 #ifndef OTH_PLY_MATH_MAX_E
 #define OTH_PLY_MATH_MAX_E 65536  // single-ply launches of at most this many boards compute their rays
 #endif
@@ -99,6 +105,13 @@ __device__ __forceinline__ uint64_t flips_rays(uint64_t P, uint64_t O, const uin
         const uint32_t s = (uint32_t)a & 63u, c = s % N;
         RayMath<N>::up(s, c, ray);
         RayMath<N>::up(N * N - 1 - s, N - 1 - c, ray + 4);
+    } else if constexpr (RAYS == RAYS_HALF) {
+        const uint64_t* rt = r - (a & 63) + ((N * N - 1 - (a & 63)) & 63);  // (in the table for any a)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            ray[d] = r[64 * d];
+            ray[4 + d] = rt[64 * d];
+        }
     } else {
 #pragma unroll
         for (int d = 0; d < 8; ++d) ray[d] = r[64 * d];
@@ -112,43 +125,6 @@ __device__ __forceinline__ uint64_t flips_rays(uint64_t P, uint64_t O, const uin
     return f | OneWord<N>::turn180(g);
 }
 
-// Per-wave W/D/L slot of a one-lane-per-board launch: slot w of the handle's
-// [nslots][4] array belongs to wave w of the grid (nslots = ceil(E / 64) covers
-// every wave holding a board; a wave past E reads the last live wave's slot and
-// never writes).  The wave's counts accumulate in SGPRs over its boards (three
-// ballots per group of 64) and lane 0 adds them with plain stores at the end.
-// Launches on a stream are ordered, so the read at a launch's start sees every
-// earlier launch's adds.
-struct WaveSlot {
-    unsigned long long* p;
-    unsigned long long v0, v1, v2;
-    uint32_t nb = 0, nd = 0, nw = 0;
-    __device__ __forceinline__ WaveSlot(unsigned long long* wdl, int t, int E) {
-        // wave-uniform: the slot is read by scalar loads into SGPRs (the values
-        // live through the whole kernel; written back by lane 0's vector stores)
-        const int w = __builtin_amdgcn_readfirstlane(min(t >> 6, (E - 1) >> 6));
-        p = wdl + 4 * (size_t)w;
-        const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(p);
-        v0 = a.x;
-        v1 = a.y;
-        v2 = p[2];
-    }
-    // {black wins, draws, white wins} of this wave's lanes (0 / 1 each)
-    __device__ __forceinline__ void count(bool b, bool d, bool w) {
-        nb += (uint32_t)__popcll(__ballot(b));
-        nd += (uint32_t)__popcll(__ballot(d));
-        nw += (uint32_t)__popcll(__ballot(w));
-    }
-    __device__ __forceinline__ void flush() const {
-        if ((nb | nd | nw) && (threadIdx.x & 63) == 0) {
-            ulonglong2 a;
-            a.x = v0 + nb;
-            a.y = v1 + nd;
-            *reinterpret_cast<ulonglong2*>(p) = a;
-            p[2] = v2 + nw;
-        }
-    }
-};
 
 // OthelloBaseEnv.step (othello.py:412-462) on a one-word board held as
 // (black B, white Wt, possible_moves L, meta m): step_lane + finish_step's
@@ -192,11 +168,14 @@ __device__ __forceinline__ void step1(uint64_t& B, uint64_t& Wt, uint64_t& L, ui
     m = (m & 0xff00u) | (new_tw ? M_TURN_WHITE : 0u) | (term ? M_TERMINATED | (wcode << M_WINNER_SHIFT) : 0u);
 }
 
-// One ply of every board, one lane per board.  A grid-stride loop with the
-// next group's loads issued before the current group's work measured slower
-// (1,048,576 boards: 15.4 -> 16.2 us per ply), and so did one streaming the
-// next group into LDS by global_load_lds while the current one computes
-// (15.1 -> 16.8 us with 16 waves per CU, 18.5 with 8).
+// One ply of every board, one lane per board.  More boards per lane (all
+// their loads issued first, each group stepped as its own loads return, the
+// stores after the last group) measured slower at 262,144 and 1,048,576 boards
+// (2 per lane +2-6 %, 4 per lane +5-17 %), and so did a grid-stride loop with
+// the next group's loads issued before the current group's work (1,048,576
+// boards: 15.4 -> 16.2 us per ply) and one streaming the next group into LDS by
+// global_load_lds while the current one computes (15.1 -> 16.8 us with 16
+// waves per CU, 18.5 with 8).
 template <int N, int SRC, int RAYS>
 __device__ __forceinline__ void ply_body(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
                                          uint64_t* __restrict__ legal, int E, uint32_t flags,
@@ -204,9 +183,10 @@ __device__ __forceinline__ void ply_body(uint64_t* __restrict__ boards, uint16_t
                                          uint8_t* __restrict__ dones, unsigned long long* __restrict__ wdl,
                                          const uint64_t* __restrict__ rays_g, Rng rng, uint64_t ply) {
     static_assert(Geo<N>::W == 1, "one-word boards");
-    static_assert(BLOCK * 2 == 8 * 64, "one 16-byte piece of the ray table per thread");
     constexpr int NN = N * N;
-    __shared__ __attribute__((aligned(16))) uint64_t rays[RAYS == RAYS_LDS ? 8 * 64 : 1];
+    constexpr int TABLE = RAYS == RAYS_LDS ? 8 * 64 : (RAYS == RAYS_HALF ? 4 * 64 : 0);  // words staged in LDS
+    static_assert(TABLE == 0 || TABLE == 2 * BLOCK || TABLE == BLOCK, "one 16- or 8-byte piece per thread");
+    __shared__ __attribute__((aligned(16))) uint64_t rays[TABLE ? TABLE : 1];
     ply += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
     const int t = blockIdx.x * BLOCK + threadIdx.x;
     const bool mine = t < E;
@@ -215,17 +195,18 @@ __device__ __forceinline__ void ply_body(uint64_t* __restrict__ boards, uint16_t
     // all (the wave then waits only for it before its LDS store), the board's
     // loads (lanes past E load board E - 1 and store nothing), the wave's slot
     ulonglong2 rv;
-    if constexpr (RAYS == RAYS_LDS) rv = reinterpret_cast<const ulonglong2*>(rays_g)[threadIdx.x];
+    uint64_t rh;
+    if constexpr (TABLE == 2 * BLOCK) rv = reinterpret_cast<const ulonglong2*>(rays_g)[threadIdx.x];
+    if constexpr (TABLE == BLOCK) rh = rays_g[threadIdx.x];  // the four up directions: the table's first half
     const ulonglong2 bw = reinterpret_cast<const ulonglong2*>(boards)[e];
     uint64_t L = legal[e];
     uint32_t m = meta[e];
     int a = 0;
     if constexpr (SRC == PLY_ACTIONS) a = actions[e];
     WaveSlot slot(wdl, t, E);
-    if constexpr (RAYS == RAYS_LDS) {
-        reinterpret_cast<ulonglong2*>(rays)[threadIdx.x] = rv;
-        __syncthreads();
-    }
+    if constexpr (TABLE == 2 * BLOCK) reinterpret_cast<ulonglong2*>(rays)[threadIdx.x] = rv;
+    if constexpr (TABLE == BLOCK) rays[threadIdx.x] = rh;
+    if constexpr (TABLE > 0) __syncthreads();
     const uint32_t id = rng.id_base + (uint32_t)e;
     uint64_t B = bw.x, Wt = bw.y;
     const bool was_term = (m & M_TERMINATED) != 0;
@@ -284,8 +265,8 @@ __global__ __launch_bounds__(BLOCK) void k_ply_step(uint64_t* __restrict__ board
                                                     const int32_t* __restrict__ actions, int32_t* __restrict__ rewards,
                                                     uint8_t* __restrict__ dones, unsigned long long* __restrict__ wdl,
                                                     const uint64_t* __restrict__ rays, Rng rng, uint64_t ply) {
-    ply_body<N, PLY_ACTIONS, RAYS>(boards, meta, legal, E, flags, const_cast<int32_t*>(actions), rewards, dones, wdl, rays,
-                             rng, ply);
+    ply_body<N, PLY_ACTIONS, RAYS>(boards, meta, legal, E, flags, const_cast<int32_t*>(actions), rewards, dones, wdl,
+                                   rays, rng, ply);
 }
 
 // oth_step_policy(RANDOM, 1 ply) on one-word boards

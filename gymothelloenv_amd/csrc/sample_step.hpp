@@ -9,10 +9,6 @@
 
 namespace oth_dev {
 
-#ifndef OTH_SS2_STEP1
-#define OTH_SS2_STEP1 0  // k_sample_step2 on one-word boards: step1 on both lanes instead of the Duo engine
-#endif
-
 // oth_sample_step: the learners' per-ply loop in one launch -- the masked
 // categorical over each board's possible_moves (Policy.act, model.py:60-99;
 // PPO.get_action, ppo.py:228-262) immediately followed by OthelloBaseEnv.step
@@ -41,6 +37,7 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step(uint64_t* __restrict__ bo
     const int l = (int)(t % G);
     const long long g0 = (t / G) * G;
     const bool mine_live = t < E;
+    WaveSlot slot(wdl, (int)t, E);
     // the board this lane steps: its loads are issued before the sampling, so
     // they are in flight while the group samples
     Lane<N> s;
@@ -92,15 +89,19 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step(uint64_t* __restrict__ bo
         if (rewards) rewards[e] = r;
         if (dones) dones[e] = (uint8_t)d;
     }
-    tally(wdl, cb, cd, cw);
+    slot.count(cb != 0, cd != 0, cw != 0);
+    slot.flush();
 }
 
-// k_sample_step on lane pairs (one-word boards): the pair samples its board
-// with oth_ms::sample_pair (bit-identical to the one-lane form) and steps it
-// with the Duo engine (half the axes and rays per lane, or-ed through DPP).
-// Twice the waves of k_sample_step for the same boards, so two waves share
-// each SIMD at 65,536 boards: the loads of one hide behind the other's VALU
-// work, and the pair halves the per-lane sampling and scanning.
+// k_sample_step on lane pairs (boards of one or two words): the pair samples
+// its board with oth_ms::sample_pair (bit-identical to the one-lane form), then
+// both lanes step it (the same inputs, so they agree): one-word boards with
+// step1 (ply.hpp: capped runs from computed rays -- no ray table, no LDS, no
+// barrier), two-word boards with the Solo engine.  Twice the waves of
+// k_sample_step for the same boards, so two waves share each SIMD at 65,536
+// boards: the loads of one hide behind the other's VALU work, and the pair
+// halves the per-lane sampling.  The W/D/L tally goes to per-wave slots
+// (ballots): no block barrier anywhere in the launch.
 template <int N, bool VEC, bool FULL>
 __global__ __launch_bounds__(BLOCK) void k_sample_step2(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
                                                         uint64_t* __restrict__ legal, int E, uint32_t flags,
@@ -115,19 +116,13 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step2(uint64_t* __restrict__ b
     constexpr int NN = N * N;
     ply += rng.ply_off[0];      // graph-region offsets (oth_graph_end); 0 eagerly
     counter += rng.ply_off[1];  // the sample counter's, as k_masked
-    // the step's engine: Duo (one-word boards: half the axes and rays per lane) or, on two-word
-    // boards, each lane the whole step (the pair's lanes agree: same inputs) without ray tables, LDS
-    // or a barrier
-    constexpr bool SOLO = W == 2;
-    constexpr bool STEP1 = W == 1 && OTH_SS2_STEP1;  // both lanes step the board with step1 (ply.hpp)
-    using Eng = typename std::conditional<SOLO, Solo<N>, Duo<N>>::type;
-    __shared__ __attribute__((aligned(16))) uint64_t lds_rays[SOLO ? 1 : 8 * 64];
     const long long gt = (long long)blockIdx.x * BLOCK + threadIdx.x;
     const int e = (int)(gt >> 1), h = (int)(gt & 1);
-    const Eng eng(h, lds_rays);
     uint32_t cb = 0, cd = 0, cw = 0;
     Lane<N> s;  // the board's loads are issued first, in flight with the logits loads
     if (e < E) load_lane<N>(s, boards, meta, legal, e);
+    // wave w of the grid owns slot w (2E lanes; the handle holds ceil(4E / 64) slots)
+    WaveSlot slot(wdl, (int)min(gt >> 6, (2LL * E - 1) >> 6));
     auto board = [&](auto STAGEDC, const oth_ms::f32x4* staged) __attribute__((always_inline)) {
         if (e >= E) return;  // pair-uniform: both lanes of a pair share e
         const oth_ms::Pick pk = oth_ms::sample_pair<W, VEC, FULL, decltype(STAGEDC)::value>(
@@ -135,12 +130,12 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step2(uint64_t* __restrict__ b
             entropy != nullptr, staged);
         const bool was_term = (s.meta & M_TERMINATED) != 0;
         int r = 0, d = 0, win = NO_DISK;
-        if constexpr (STEP1) {
+        if constexpr (W == 1) {
             uint64_t B = s.black.w[0], Wt = s.white.w[0], L = s.legal.w[0];
             uint32_t m = s.meta;
             const int a = pk.a;
             const bool valid = (unsigned)a < (unsigned)NN && ((L >> (a & 63)) & 1ull);
-            step1<N>(B, Wt, L, m, a, valid, flags, lds_rays, r, d, win);
+            step1<N, RAYS_MATH>(B, Wt, L, m, a, valid, flags, nullptr, r, d, win);
             if (was_term) {  // a no-op reporting done (othello.py:415-416)
                 r = 0;
                 d = 1;
@@ -151,7 +146,7 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step2(uint64_t* __restrict__ b
                 s.meta = m;
             }
         } else {
-            step_lane<N>(s, pk.a, flags, r, d, win, eng);
+            step_lane<N>(s, pk.a, flags, r, d, win, Solo<N>(0, nullptr));
         }
         if (d && !was_term) {
             if (h == 0) {
@@ -171,21 +166,19 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step2(uint64_t* __restrict__ b
             if (dones) dones[e] = (uint8_t)d;
         }
     };
-    // the ray tables are built after the loads are issued (their latency hides the build)
     if constexpr (VEC && N == 8 && OTH_SS2_STAGE) {  // the wave's 32 rows through LDS: coalesced loads
         __shared__ oth_ms::f32x4 stage[(BLOCK / 64) * 32 * oth_ms::PAIR_ROW];
         const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
         oth_ms::f32x4 v[8];
         oth_ms::load_pair_rows(v, (gt - lane) >> 1, E, logits, ld, lane);
-        if constexpr (!SOLO) fill_rays<N, STEP1, false>(lds_rays);  // while the rows are in flight
+        // (store_pair_rows syncs the wave: each wave reads back only its own rows)
         const oth_ms::f32x4* rows = oth_ms::store_pair_rows(stage + wv * 32 * oth_ms::PAIR_ROW, v, lane);
-        __syncthreads();  // the ray tables (the rows need only the wave's own order)
         board(std::true_type{}, rows);
     } else {
-        if constexpr (!SOLO) fill_rays<N, STEP1>(lds_rays);
         board(std::false_type{}, nullptr);
     }
-    tally(wdl, cb, cd, cw);
+    slot.count(cb != 0, cd != 0, cw != 0);  // (h == 0 lanes only)
+    slot.flush();
 }
 
 // k_sample_step on lane quads (one-word boards): the quad IS k_masked's group
@@ -211,6 +204,7 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step4(uint64_t* __restrict__ b
     const int e = (int)(gt >> 2), q = (int)(gt & 3);
     const Quartet<N> eng(q, lds_rays);
     uint32_t cb = 0, cd = 0, cw = 0;
+    WaveSlot slot(wdl, (int)min(gt >> 6, (4LL * E - 1) >> 6));  // 4E lanes: ceil(4E / 64) slots
     Lane<N> s;  // the board's and the logits' loads are issued before the ray tables are built
     oth_ms::Slot<1, 4> b;
     b.e = e;
@@ -245,7 +239,8 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step4(uint64_t* __restrict__ b
             if (dones) dones[e] = (uint8_t)d;
         }
     }
-    tally(wdl, cb, cd, cw);
+    slot.count(cb != 0, cd != 0, cw != 0);  // (q == 0 lanes only)
+    slot.flush();
 }
 
 }  // namespace oth_dev

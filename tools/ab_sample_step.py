@@ -42,8 +42,10 @@ def main():
     rew = torch.empty(E, dtype=torch.int32, device=dev)
     don = torch.empty(E, dtype=torch.uint8, device=dev)
     ref = None
+    print("torch up", file=sys.stderr, flush=True)
     for nm in a.names:
         lib = L.load_path(os.path.join(VDIR, "liboth_%s.so" % nm))
+        print("variant %s loaded" % nm, file=sys.stderr, flush=True)
         env = VecOthelloEnv(E, board_size=n, auto_reset=True, seed=0, device=dev, lib=lib)
         env.reset()
 
@@ -63,8 +65,10 @@ def main():
             for k in range(K):
                 ply(env, k)
         envs[nm], graphs[nm] = env, graph
+        print("variant %s ready" % nm, file=sys.stderr, flush=True)
     times = {nm: [] for nm in a.names}
-    for _ in range(a.rounds):
+    for rd in range(a.rounds):
+        print("round %d" % rd, file=sys.stderr, flush=True)
         for nm in a.names:
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

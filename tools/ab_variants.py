@@ -19,12 +19,13 @@ sys.path.insert(0, ROOT)
 VDIR = os.path.join(ROOT, "gymothelloenv_amd", "variants")
 
 
-def build(specs):
+def build(specs, sizes=None):
     from gymothelloenv_amd import build as hb
     os.makedirs(VDIR, exist_ok=True)
     for spec in specs:
         name, _, flags = spec.partition("=")
-        hb.build(force=True, extra_flags=flags.split(), out=os.path.join(VDIR, "liboth_%s.so" % name))
+        hb.build(force=True, extra_flags=flags.split(), out=os.path.join(VDIR, "liboth_%s.so" % name),
+                 only_sizes=sizes)
 
 
 def run(names, E, n, plies, launches, rounds, policy, check=True, init_rand=0):
@@ -87,9 +88,10 @@ def main():
     ap.add_argument("--policy", default="random")
     ap.add_argument("--init-rand", type=int, default=0, help="random-opening bound (initial_rand_steps)")
     ap.add_argument("--no-check", action="store_true", help="timing ablations: outputs differ by design")
+    ap.add_argument("--sizes", help="--build: compile only these board sizes' units (e.g. 8), link the rest from the main build")
     a = ap.parse_args()
     if a.build:
-        build(a.build)
+        build(a.build, [int(x) for x in a.sizes.split(",")] if a.sizes else None)
     if a.run:
         run(a.run, a.envs, a.board_size, a.plies, a.launches, a.rounds, a.policy, check=not a.no_check,
             init_rand=a.init_rand)
