@@ -87,12 +87,6 @@ using namespace oth;
 #ifndef OTH_OBS_WAVE
 #define OTH_OBS_WAVE 1  // observations: one wave per 64 boards (k_observe_w) instead of one board per wave (k_observe_q)
 #endif
-#ifndef OTH_RAND_FILL
-#define OTH_RAND_FILL 1  // k_play_rand: the next Philox block computed after the first ply's scan (its region)
-#endif
-#ifndef OTH_RAND_PIPE
-#define OTH_RAND_PIPE 1  // k_play_rand: the next Philox block computed inside the current 4-ply group
-#endif
 #ifndef OTH_SS_PAIR
 #define OTH_SS_PAIR 1  // oth_sample_step on lane pairs for one-word boards (k_sample_step2)
 #endif
@@ -1229,7 +1223,7 @@ __device__ __forceinline__ void tally_from_signs(uint32_t s, uint32_t g, uint32_
 }
 // FILL: independent work (the next Philox block) run after the opponent's scan
 // and pinned there, so that it shares the ply's first scheduling region with the
-// pick, the ray-table loads, the flips and the scan (OTH_RAND_FILL)
+// pick, the ray-table loads, the flips and the scan
 template <int N, int POLICY = OTH_POLICY_RANDOM, bool OPEN = true, typename Eng = Fills<N>, typename FILL = NoFill>
 __device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_t& L, uint32_t& meta,
                                                const Eng& eng, uint32_t u, uint32_t flags, const Rng& rng,
@@ -1275,6 +1269,11 @@ __device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_
         Ln = eng.legal(pb, ob).w[0];
     }
     const bool term = full || Ln == 0;  // full board or nobody can move (:441-442)
+    // (M, O) := (next mover, its opponent).  Alternating the two words' roles
+    // statically from ply to ply instead (no selects; a pass swapping them in its
+    // own exec-masked block) measured 2.3 % slower; per-ply outputs through buffer descriptors (no 64-bit
+    // address VALU) 2.3 % slower too, their descriptor SALU in the same issue stream
+    // (profiles/r03/st/)
     const bool swap = !pass && !full;
     M = swap ? On : Mn;
     O = swap ? Mn : On;
@@ -1381,10 +1380,10 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
             return;
         }
         int p = 0;
-#if OTH_RAND_PIPE
             // Philox block g/4 serves plies 4k..4k+3 (g uniform: scalar branches).
-            // The next block is computed in the current group's first ply, where
-            // its independent VALU work fills the wait for the ray-table loads.
+            // The next block is computed in the current group's first ply, after its
+            // opponent scan and pinned there (FILL), where its independent VALU
+            // work shares the ply's scheduling region (profiles/r02/fi/).
             while (p < plies && ((ply0 + (uint64_t)p) & 3) != 0) {
                 const uint64_t g = ply0 + (uint64_t)p;
                 ply(p, pick4(philox4(rng.seed, id, g >> 2, RNG_ACTION), (uint32_t)(g & 3)), nofill);
@@ -1393,20 +1392,12 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
             if (p + 4 <= plies) {
                 U4 cur = philox4(rng.seed, id, (ply0 + (uint64_t)p) >> 2, RNG_ACTION);
                 while (p + 4 <= plies) {
-#if OTH_RAND_FILL
-                    // the next block (one unused after the last group) computed in the first
-                    // ply's region, pinned before its pass test
-                    U4 nxt;
+                    U4 nxt;  // (one unused block after the last group)
                     const uint64_t nb = ((ply0 + (uint64_t)p) >> 2) + 1;
                     ply(p, cur.x, [&]() __attribute__((always_inline)) {
                         nxt = philox4(rng.seed, id, nb, RNG_ACTION);
                         asm volatile("" : "+v"(nxt.x), "+v"(nxt.y), "+v"(nxt.z), "+v"(nxt.w));
                     });
-#else
-                    const U4 nxt = p + 8 <= plies ? philox4(rng.seed, id, ((ply0 + (uint64_t)p) >> 2) + 1, RNG_ACTION)
-                                                  : cur;
-                    ply(p, cur.x, nofill);
-#endif
                     ply(p + 1, cur.y, nofill);
                     ply(p + 2, cur.z, nofill);
                     ply(p + 3, cur.w, nofill);
@@ -1419,22 +1410,6 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
                 ply(p, pick4(philox4(rng.seed, id, g >> 2, RNG_ACTION), (uint32_t)(g & 3)), nofill);
                 ++p;
             }
-#else
-            while (p < plies) {  // Philox block g/4 serves plies 4k..4k+3 (g uniform: scalar branches)
-                const uint64_t g = ply0 + (uint64_t)p;
-                const U4 d4 = philox4(rng.seed, id, g >> 2, RNG_ACTION);
-                if ((g & 3) == 0 && p + 4 <= plies) {
-                    ply(p, d4.x, nofill);
-                    ply(p + 1, d4.y, nofill);
-                    ply(p + 2, d4.z, nofill);
-                    ply(p + 3, d4.w, nofill);
-                    p += 4;
-                } else {
-                    ply(p, pick4(d4, (uint32_t)(g & 3)), nofill);
-                    ++p;
-                }
-            }
-#endif
         };
         if (!slow) {
             // no opening bookkeeping when no board of the wave can have opening plies

@@ -70,7 +70,7 @@ int launch_step(oth_env* env, const int32_t* actions, int32_t* rewards, uint8_t*
                                env->meta, env->legal, env->E, env->flags, actions, rewards, dones, env->wdl, env->rays,
                                rng_of(env), ply);
         else
-            hipLaunchKernelGGL((k_ply_step<N, OTH_PLY_BIG_RAYS>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st,
+            hipLaunchKernelGGL((k_ply_step<N, RAYS_HALF>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st,
                                env->boards, env->meta, env->legal, env->E, env->flags, actions, rewards, dones,
                                env->wdl, env->rays, rng_of(env), ply);
         return after_launch("oth_step");
@@ -93,7 +93,7 @@ void launch_k_play(int lanes_per_board, oth_env* env, int policy, int n_plies, i
                                    env->meta, env->legal, env->E, env->flags, actions, rewards, dones, env->wdl,
                                    env->rays, rng_of(env), ply0);
             else
-                hipLaunchKernelGGL((k_ply_rand<N, OTH_PLY_BIG_RAYS>), dim3(grid_for(env->E)), block, 0, st,
+                hipLaunchKernelGGL((k_ply_rand<N, RAYS_HALF>), dim3(grid_for(env->E)), block, 0, st,
                                    env->boards, env->meta, env->legal, env->E, env->flags, actions, rewards, dones,
                                    env->wdl, env->rays, rng_of(env), ply0);
             return;

@@ -4,7 +4,7 @@
 // (build.py PLAY_FLAGS: -mllvm -amdgpu-sched-strategy=max-ilp).  At 65,536
 // boards each SIMD runs one wave, so what the schedule hides of the dependent
 // chains counts and occupancy does not: 8x8 0.779 -> 0.762 us per ply with
-// OTH_RAND_FILL (profiles/r02/fi/).  The same flag on the whole library costs
+// the next Philox block pinned in the group's first ply (profiles/r02/fi/).  The same flag on the whole library costs
 // the fused sample-and-step kernel 4 %, hence the separate unit.
 #include "device.hpp"
 #include "launch.hpp"

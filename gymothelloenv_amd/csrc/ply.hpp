@@ -10,11 +10,12 @@
 //   * every load a lane needs (board, possible_moves, flags, action, the
 //     wave's W/D/L slot) is issued first and unconditionally (lanes past E load
 //     board E - 1 and store nothing), so one memory latency is paid, not two;
-//   * update_board's flips come from a ray table (the handle's 4 KiB table in
-//     device memory, staged in LDS by one 16-byte load per thread issued before
-//     the boards' loads) with the capping test of the nearest non-opponent
-//     square: about 60 VALU and eight LDS reads for the eight directions against
-//     about 260 VALU for Kogge-Stone runs from the square;
+//   * update_board's flips are capped runs along the eight rays of the square
+//     (the nearest non-opponent square, one 3-input op per dword for the cap
+//     test): about 90 VALU against about 260 for Kogge-Stone runs from the
+//     square; the rays are computed (small launches) or read from the up half
+//     of the handle's ray table staged in LDS by one 8-byte load per thread
+//     issued before the boards' loads (large launches);
 //   * the reset position's possible_moves is a compile-time constant;
 //   * the W/D/L tally is per wave: three ballots, and lane 0 adds their counts
 //     to the wave's own slot with plain stores (read with the board loads) --
@@ -32,18 +33,16 @@ constexpr int PLY_ACTIONS = 0, PLY_RANDOM = 1;
 #endif
 
 // Where the flips' rays come from (a template parameter of the single-ply kernels):
-//   RAYS_LDS   the handle's table staged in LDS (fewest VALU: faster where the
-//              launch is bandwidth-bound, 1,048,576 boards 15.8 -> 14.9 us per ply)
 //   RAYS_MATH  computed per move, no table, no LDS, no barrier (+32 VALU: faster
 //              where one wave per SIMD runs a latency-bound chain, 65,536
-//              boards 3.37 -> 3.11 us per ply; profiles/r03/ab/ab_blocks.jsonl)
-//   RAYS_HALF  the table's four up directions staged in LDS (8 bytes per thread,
-//              half the table traffic); a turned down ray of square a is the up
-//              ray of square NN-1-a (RayMath below)
-constexpr int RAYS_LDS = 1, RAYS_MATH = 2, RAYS_HALF = 3;
-#ifndef OTH_PLY_BIG_RAYS
-#define OTH_PLY_BIG_RAYS RAYS_LDS  // the ray source of single-ply launches above OTH_PLY_MATH_MAX_E boards
-#endif
+//              boards 3.37 -> 3.11 us per ply against the whole table in LDS;
+//              profiles/r03/ab/ab_blocks.jsonl)
+//   RAYS_HALF  the four up directions of the handle's table staged in LDS, 8
+//              bytes per thread; a turned down ray of square a is the up ray of
+//              square NN-1-a (RayMath below).  Against the whole table (16 bytes
+//              per thread): 262,144 boards 5.79 -> 5.45 us per ply, 1,048,576
+//              13.32 -> 13.12 (profiles/r03/ply/ab_half_table.jsonl)
+constexpr int RAYS_MATH = 2, RAYS_HALF = 3;
 #ifndef OTH_PLY_MATH_MAX_E
 #define OTH_PLY_MATH_MAX_E 65536  // single-ply launches of at most this many boards compute their rays
 #endif
@@ -105,16 +104,14 @@ __device__ __forceinline__ uint64_t flips_rays(uint64_t P, uint64_t O, const uin
         const uint32_t s = (uint32_t)a & 63u, c = s % N;
         RayMath<N>::up(s, c, ray);
         RayMath<N>::up(N * N - 1 - s, N - 1 - c, ray + 4);
-    } else if constexpr (RAYS == RAYS_HALF) {
+    } else {
+        static_assert(RAYS == RAYS_HALF, "ray source");
         const uint64_t* rt = r - (a & 63) + ((N * N - 1 - (a & 63)) & 63);  // (in the table for any a)
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
             ray[d] = r[64 * d];
             ray[4 + d] = rt[64 * d];
         }
-    } else {
-#pragma unroll
-        for (int d = 0; d < 8; ++d) ray[d] = r[64 * d];
     }
     uint64_t f = 0, g = 0;
 #pragma unroll
@@ -131,7 +128,7 @@ __device__ __forceinline__ uint64_t flips_rays(uint64_t P, uint64_t O, const uin
 // decisions, branch-free except the pass re-scan (taken by the wave only when
 // one of its lanes passes).  valid: the action is in possible_moves (`a` in
 // [0, N*N) then).  Returns reward / done / winner (0 unless the game ended).
-template <int N, int RAYS = RAYS_LDS>
+template <int N, int RAYS = RAYS_MATH>
 __device__ __forceinline__ void step1(uint64_t& B, uint64_t& Wt, uint64_t& L, uint32_t& m, int a, bool valid,
                                       uint32_t flags, const uint64_t* __restrict__ rays, int& reward, int& done,
                                       int& winner) {
@@ -184,8 +181,8 @@ __device__ __forceinline__ void ply_body(uint64_t* __restrict__ boards, uint16_t
                                          const uint64_t* __restrict__ rays_g, Rng rng, uint64_t ply) {
     static_assert(Geo<N>::W == 1, "one-word boards");
     constexpr int NN = N * N;
-    constexpr int TABLE = RAYS == RAYS_LDS ? 8 * 64 : (RAYS == RAYS_HALF ? 4 * 64 : 0);  // words staged in LDS
-    static_assert(TABLE == 0 || TABLE == 2 * BLOCK || TABLE == BLOCK, "one 16- or 8-byte piece per thread");
+    constexpr int TABLE = RAYS == RAYS_HALF ? 4 * 64 : 0;  // words staged in LDS
+    static_assert(TABLE == 0 || TABLE == BLOCK, "one 8-byte piece of the table per thread");
     __shared__ __attribute__((aligned(16))) uint64_t rays[TABLE ? TABLE : 1];
     ply += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
     const int t = blockIdx.x * BLOCK + threadIdx.x;
@@ -194,19 +191,18 @@ __device__ __forceinline__ void ply_body(uint64_t* __restrict__ boards, uint16_t
     // every load first, none behind a branch: the ray table's piece first of
     // all (the wave then waits only for it before its LDS store), the board's
     // loads (lanes past E load board E - 1 and store nothing), the wave's slot
-    ulonglong2 rv;
     uint64_t rh;
-    if constexpr (TABLE == 2 * BLOCK) rv = reinterpret_cast<const ulonglong2*>(rays_g)[threadIdx.x];
-    if constexpr (TABLE == BLOCK) rh = rays_g[threadIdx.x];  // the four up directions: the table's first half
+    if constexpr (TABLE) rh = rays_g[threadIdx.x];  // the four up directions: the table's first half
     const ulonglong2 bw = reinterpret_cast<const ulonglong2*>(boards)[e];
     uint64_t L = legal[e];
     uint32_t m = meta[e];
     int a = 0;
     if constexpr (SRC == PLY_ACTIONS) a = actions[e];
     WaveSlot slot(wdl, t, E);
-    if constexpr (TABLE == 2 * BLOCK) reinterpret_cast<ulonglong2*>(rays)[threadIdx.x] = rv;
-    if constexpr (TABLE == BLOCK) rays[threadIdx.x] = rh;
-    if constexpr (TABLE > 0) __syncthreads();
+    if constexpr (TABLE) {
+        rays[threadIdx.x] = rh;
+        __syncthreads();
+    }
     const uint32_t id = rng.id_base + (uint32_t)e;
     uint64_t B = bw.x, Wt = bw.y;
     const bool was_term = (m & M_TERMINATED) != 0;

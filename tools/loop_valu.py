@@ -30,6 +30,10 @@ def valu(lines, a, b):
     return sum(1 for l in lines[a:b] if re.match(r"\s+v_", l))
 
 
+def salu(lines, a, b):
+    return sum(1 for l in lines[a:b] if re.match(r"\s+s_", l) and not re.match(r"\s+s_(waitcnt|nop|cbranch|branch)", l))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("asm")
@@ -54,8 +58,8 @@ def main():
         i += 1
     tot = valu(L, start, end)
     cond = sum(valu(L, x, y) for x, y in regions)
-    print("loop .LBB%s lines %d-%d: VALU %d, always %d, exec-masked regions %s" % (
-        key, start, end, tot, tot - cond, [valu(L, x, y) for x, y in regions]))
+    print("loop .LBB%s lines %d-%d: VALU %d, always %d, exec-masked regions %s; SALU %d" % (
+        key, start, end, tot, tot - cond, [valu(L, x, y) for x, y in regions], salu(L, start, end)))
 
 
 if __name__ == "__main__":
