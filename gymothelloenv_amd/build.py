@@ -3,7 +3,7 @@ travels with the repo snapshot to the GPU box).
 
 The kernels are templates over the board size N; csrc/kernels_n.hip is
 compiled once per N (-DOTH_N=4..16) in parallel, csrc/play_rand_n.hip (the
-bench kernel, its own scheduler flags) once per N = 4..8, csrc/capi.hip holds
+fused random-play kernels, its own scheduler flags) once per N = 4..11, csrc/capi.hip holds
 the C ABI, and the objects are linked into one shared library.
 
 Reproducibility: objects go to a fixed directory (`_objs/`, git-ignored) so the
@@ -26,10 +26,12 @@ CSRC = os.path.join(HERE, "csrc")
 SIZES = list(range(4, 17))
 SOURCES = ("capi.hip", "kernels_n.hip", "play_rand_n.hip", "masked.hip", "device.hpp", "launch.hpp", "bitboard.hpp",
            "masked.hpp", "ply.hpp", "sample_step.hpp")
-PLAY_SIZES = list(range(4, 9))  # k_play_rand: one-word boards
+PLAY_SIZES = list(range(4, 12))  # k_play_rand (one-word boards) and k_play_rand_w (two-word boards)
 # play_rand_n.hip: the max-ILP machine scheduler (one wave per SIMD: latency hidden by the schedule
 # counts, occupancy does not); the rest of the library keeps the default scheduler
 PLAY_FLAGS = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
+if os.environ.get("OTH_PLAY_FLAGS") is not None:  # A/B variants of the tools only (the hash records the flags)
+    PLAY_FLAGS = os.environ["OTH_PLAY_FLAGS"].split()
 DEPS = [os.path.join(CSRC, f) for f in SOURCES] + [os.path.join(ROOT, "include", "othello_mi355x.h")]
 OUT = os.path.join(HERE, "liboth_mi355x.so")
 OBJDIR = os.path.join(HERE, "_objs")

@@ -1455,11 +1455,12 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
 // play_rand_fast for multi-word boards (N >= 9, the FillsW engine): the same
 // (mover, opponent) form with BB<W> words; every multi-word select is word by
 // word (a selected member address puts the lane in scratch).
-template <int N>
+template <int N, typename FILL = NoFill>
 __device__ __forceinline__ void play_rand_fast_w(BB<Geo<N>::W>& M, BB<Geo<N>::W>& O, BB<Geo<N>::W>& L,
                                                  uint32_t& meta, const FillsW<N>& eng, uint32_t u, uint32_t flags,
                                                  const Rng& rng, uint32_t id, uint64_t g, int& a, int& r, int& d,
-                                                 uint32_t& cb, uint32_t& cd, uint32_t& cw, const uint8_t* sel8) {
+                                                 uint32_t& cb, uint32_t& cd, uint32_t& cw, const uint8_t* sel8,
+                                                 const FILL& fill = FILL{}) {
     constexpr int W = Geo<N>::W;
     constexpr int NN = N * N;
 #if OTH_SELECT_LDS
@@ -1474,6 +1475,7 @@ __device__ __forceinline__ void play_rand_fast_w(BB<Geo<N>::W>& M, BB<Geo<N>::W>
     const BB<W> Mn = M | f | m, On = O & ~f;
     const bool full = !any(~(Mn | On) & Geo<N>::BOARD);  // :425-426
     BB<W> Ln = eng.legal(On, Mn);                          // the opponent's possible_moves (:436)
+    fill();
     const bool pass = !any(Ln) && !full;
     if (pass) Ln = eng.legal(Mn, On);  // :437-440
     const bool term = full || !any(Ln);
@@ -1559,9 +1561,9 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand_w(uint64_t* __restrict__ bo
 #else
         uint32_t &t0 = cb, &t1 = cd, &t2 = cw;
 #endif
-        auto ply = [&](uint64_t g, uint32_t u) __attribute__((always_inline)) {
+        auto ply = [&](uint64_t g, uint32_t u, const auto& fill) __attribute__((always_inline)) {
             int a, r, d;
-            play_rand_fast_w<N>(M, O, L, mt, eng, u, flags, rng, id, g, a, r, d, t0, t1, t2, sel8);
+            play_rand_fast_w<N>(M, O, L, mt, eng, u, flags, rng, id, g, a, r, d, t0, t1, t2, sel8, fill);
             *act_p = a;
             *rew_p = r;
             *done_p = (uint8_t)d;
@@ -1570,18 +1572,52 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand_w(uint64_t* __restrict__ bo
             done_p += E;
         };
         if (!slow) {
+            // Philox block g/4 serves plies 4k..4k+3 (g uniform: scalar branches).
+            // Two-word boards compute the next block in the current group's first ply
+            // (as k_play_rand: 10x10 +5 %); boards of 3+ words, already past 256 VGPRs,
+            // at each group's start (the pipelined form: 12x12 -4 %)
+            const NoFill nofill;
             int p = 0;
-            while (p < plies) {  // Philox block g/4 serves plies 4k..4k+3 (g uniform: scalar branches)
-                const uint64_t g = ply0 + (uint64_t)p;
-                const U4 d4 = philox4(rng.seed, id, g >> 2, RNG_ACTION);
-                if ((g & 3) == 0 && p + 4 <= plies) {
-                    ply(g, d4.x);
-                    ply(g + 1, d4.y);
-                    ply(g + 2, d4.z);
-                    ply(g + 3, d4.w);
-                    p += 4;
-                } else {
-                    ply(g, pick4(d4, (uint32_t)(g & 3)));
+            if constexpr (W > 2) {
+                while (p < plies) {
+                    const uint64_t g = ply0 + (uint64_t)p;
+                    const U4 d4 = philox4(rng.seed, id, g >> 2, RNG_ACTION);
+                    if ((g & 3) == 0 && p + 4 <= plies) {
+                        ply(g, d4.x, nofill);
+                        ply(g + 1, d4.y, nofill);
+                        ply(g + 2, d4.z, nofill);
+                        ply(g + 3, d4.w, nofill);
+                        p += 4;
+                    } else {
+                        ply(g, pick4(d4, (uint32_t)(g & 3)), nofill);
+                        ++p;
+                    }
+                }
+            } else {
+                while (p < plies && ((ply0 + (uint64_t)p) & 3) != 0) {
+                    const uint64_t g = ply0 + (uint64_t)p;
+                    ply(g, pick4(philox4(rng.seed, id, g >> 2, RNG_ACTION), (uint32_t)(g & 3)), nofill);
+                    ++p;
+                }
+                if (p + 4 <= plies) {
+                    U4 cur = philox4(rng.seed, id, (ply0 + (uint64_t)p) >> 2, RNG_ACTION);
+                    while (p + 4 <= plies) {
+                        const uint64_t g = ply0 + (uint64_t)p;
+                        U4 nxt;  // (one unused block after the last group)
+                        ply(g, cur.x, [&]() __attribute__((always_inline)) {
+                            nxt = philox4(rng.seed, id, (g >> 2) + 1, RNG_ACTION);
+                            asm volatile("" : "+v"(nxt.x), "+v"(nxt.y), "+v"(nxt.z), "+v"(nxt.w));
+                        });
+                        ply(g + 1, cur.y, nofill);
+                        ply(g + 2, cur.z, nofill);
+                        ply(g + 3, cur.w, nofill);
+                        cur = nxt;
+                        p += 4;
+                    }
+                }
+                while (p < plies) {
+                    const uint64_t g = ply0 + (uint64_t)p;
+                    ply(g, pick4(philox4(rng.seed, id, g >> 2, RNG_ACTION), (uint32_t)(g & 3)), nofill);
                     ++p;
                 }
             }

@@ -113,8 +113,11 @@ void launch_k_play(int lanes_per_board, oth_env* env, int policy, int n_plies, i
     }
     if constexpr (OTH_FAST_RANDOM_W && POL == OTH_POLICY_RANDOM && std::is_same<Eng, FillsW<N>>::value) {
         if (actions && rewards && dones && (env->flags & OTH_AUTO_RESET)) {
-            hipLaunchKernelGGL((k_play_rand_w<N>), grid, block, 0, st, env->boards, env->meta, env->legal, env->E,
-                               env->flags, n_plies, actions, rewards, dones, env->wdl, rng_of(env, policy), ply0);
+            if constexpr (Geo<N>::W == 2)  // the max-ILP unit (play_rand_n.hip): 10x10 +5 %, 12x12 -4 %
+                launch_play_rand<N, OTH_POLICY_RANDOM>(env, n_plies, actions, rewards, dones, ply0, st);
+            else
+                hipLaunchKernelGGL((k_play_rand_w<N>), grid, block, 0, st, env->boards, env->meta, env->legal, env->E,
+                                   env->flags, n_plies, actions, rewards, dones, env->wdl, rng_of(env, policy), ply0);
             return;
         }
     }

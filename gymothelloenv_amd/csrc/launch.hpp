@@ -73,7 +73,8 @@ template <int N> int launch_observe(oth_env* env, int layout, int dtype, void* o
 template <int N> int launch_set_turn(oth_env* env, int turn, const uint8_t* mask, hipStream_t st);
 template <int N> int launch_count(oth_env* env, int32_t* out, hipStream_t st);
 template <int N> int launch_fill_rays(oth_env* env, hipStream_t st);
-// k_play_rand for one-word boards (play_rand_n.hip, N = 4..8, its own scheduler flags)
+// k_play_rand (one-word boards, random and greedy) and k_play_rand_w (two-word boards,
+// random) in play_rand_n.hip, N = 4..11, with its own scheduler flags
 template <int N, int POL>
 void launch_play_rand(oth_env* env, int n_plies, int32_t* actions, int32_t* rewards, uint8_t* dones, uint64_t ply0,
                       hipStream_t st);

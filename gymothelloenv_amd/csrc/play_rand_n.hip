@@ -1,6 +1,7 @@
 // play_rand_n.hip -- k_play_rand (the restructured random / greedy play of
-// one-word boards, the bench kernel) in a translation unit of its own per board
-// size (-DOTH_N=4 .. 8), compiled with the max-ILP machine scheduler
+// one-word boards, the bench kernel) and k_play_rand_w (random play of
+// multi-word boards) in a translation unit of their own per board size
+// (-DOTH_N=4 .. 16), compiled with the max-ILP machine scheduler
 // (build.py PLAY_FLAGS: -mllvm -amdgpu-sched-strategy=max-ilp).  At 65,536
 // boards each SIMD runs one wave, so what the schedule hides of the dependent
 // chains counts and occupancy does not: 8x8 0.779 -> 0.762 us per ply with
@@ -21,16 +22,21 @@ namespace oth_host {
 template <int N, int POL>
 void launch_play_rand(oth_env* env, int n_plies, int32_t* actions, int32_t* rewards, uint8_t* dones, uint64_t ply0,
                       hipStream_t st) {
-    static_assert(Geo<N>::W == 1, "k_play_rand is for one-word boards");
     const dim3 grid((unsigned)(((long long)env->E + BLOCK - 1) / BLOCK)), block(BLOCK);
     const Rng rng{env->seed, env->id_base, env->init_rand, env->cur_off};
-    hipLaunchKernelGGL((k_play_rand<N, POL>), grid, block, 0, st, env->boards, env->meta, env->legal, env->E,
-                       env->flags, n_plies, actions, rewards, dones, env->wdl, rng, ply0);
+    if constexpr (Geo<N>::W == 1)
+        hipLaunchKernelGGL((k_play_rand<N, POL>), grid, block, 0, st, env->boards, env->meta, env->legal, env->E,
+                           env->flags, n_plies, actions, rewards, dones, env->wdl, rng, ply0);
+    else  // random play only (k_play_rand_w)
+        hipLaunchKernelGGL((k_play_rand_w<N>), grid, block, 0, st, env->boards, env->meta, env->legal, env->E,
+                           env->flags, n_plies, actions, rewards, dones, env->wdl, rng, ply0);
 }
 
 template void launch_play_rand<OTH_N, OTH_POLICY_RANDOM>(oth_env*, int, int32_t*, int32_t*, uint8_t*, uint64_t,
                                                          hipStream_t);
+#if OTH_N <= 8
 template void launch_play_rand<OTH_N, OTH_POLICY_GREEDY>(oth_env*, int, int32_t*, int32_t*, uint8_t*, uint64_t,
                                                          hipStream_t);
+#endif
 
 }  // namespace oth_host
