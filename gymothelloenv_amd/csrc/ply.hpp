@@ -43,9 +43,6 @@ constexpr int PLY_ACTIONS = 0, PLY_RANDOM = 1;
 //              per thread): 262,144 boards 5.79 -> 5.45 us per ply, 1,048,576
 //              13.32 -> 13.12 (profiles/r03/ply/ab_half_table.jsonl)
 constexpr int RAYS_MATH = 2, RAYS_HALF = 3;
-#ifndef OTH_PLY_NT
-#define OTH_PLY_NT 0  // probe: nontemporal stores in the large single-ply launches
-#endif
 #ifndef OTH_PLY_MATH_MAX_E
 #define OTH_PLY_MATH_MAX_E 65536  // single-ply launches of at most this many boards compute their rays
 #endif
@@ -185,7 +182,10 @@ __device__ __forceinline__ void ply_body(uint64_t* __restrict__ boards, uint16_t
     static_assert(Geo<N>::W == 1, "one-word boards");
     constexpr int NN = N * N;
     constexpr int TABLE = RAYS == RAYS_HALF ? 4 * 64 : 0;  // words staged in LDS
-    constexpr bool NT = RAYS == RAYS_HALF;  // (the large launches)
+    // the large launches store nontemporally (streaming, no L2 allocation): 262,144
+    // boards 5.85 -> 5.50 us per ply, 1,048,576 13.32 -> 12.78; the small ones gain
+    // nothing from it (profiles/r03/nt/)
+    constexpr bool NT = RAYS == RAYS_HALF;
     static_assert(TABLE == 0 || TABLE == BLOCK, "one 8-byte piece of the table per thread");
     __shared__ __attribute__((aligned(16))) uint64_t rays[TABLE ? TABLE : 1];
     ply += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
@@ -244,15 +244,12 @@ __device__ __forceinline__ void ply_body(uint64_t* __restrict__ boards, uint16_t
             ulonglong2 o;
             o.x = B;
             o.y = Wt;
-#if OTH_PLY_NT
-            if (NT) {  // streaming stores of large launches (OTH_PLY_NT probe)
+            if (NT) {
                 __builtin_nontemporal_store(o.x, &boards[2 * (size_t)e]);
                 __builtin_nontemporal_store(o.y, &boards[2 * (size_t)e + 1]);
                 __builtin_nontemporal_store(L, &legal[e]);
                 __builtin_nontemporal_store((uint16_t)m, &meta[e]);
-            } else
-#endif
-            {
+            } else {
                 reinterpret_cast<ulonglong2*>(boards)[e] = o;
                 legal[e] = L;
                 meta[e] = (uint16_t)m;
@@ -260,13 +257,10 @@ __device__ __forceinline__ void ply_body(uint64_t* __restrict__ boards, uint16_t
         }
         if constexpr (SRC == PLY_RANDOM)
             if (actions) actions[e] = a;
-#if OTH_PLY_NT
         if (NT) {
             if (rewards) __builtin_nontemporal_store(r, &rewards[e]);
             if (dones) __builtin_nontemporal_store((uint8_t)d, &dones[e]);
-        } else
-#endif
-        {
+        } else {
             if (rewards) rewards[e] = r;
             if (dones) dones[e] = (uint8_t)d;
         }
