@@ -607,7 +607,8 @@ def test_single_ply_kernels_both_ray_sources(torch_cuda, n, E):
     """The single-ply kernels (ply.hpp) compute their rays up to 65,536 boards
     and read the handle's LDS-staged table beyond: both equal the oracle for
     external actions (legal, illegal, out of range; both sudden-death modes)
-    and for one-ply random play, ragged E included."""
+    and for one-ply random play, ragged E included; dones views at every byte
+    offset (the kernels pack a lane quad's dones into one dword when aligned)."""
     torch = torch_cuda
     rng = np.random.RandomState(E + n)
     for sd in (True, False):
@@ -619,9 +620,13 @@ def test_single_ply_kernels_both_ray_sources(torch_cuda, n, E):
             wild = (rng.rand(E) < 0.1) | ~lb.any(axis=1)
             acts = np.where(wild, rng.randint(-2, n * n + 2, size=E), pick).astype(np.int32)
             orw, od, _ = oracle.step(s, flags_of(sd, False, True), acts, seed=9, ply=p)
-            _, rew, dn, _ = env.step(torch.from_numpy(acts).cuda(), observe=False)
+            off = p % 4  # dones at every byte offset (packed dword stores only where 4-aligned)
+            dbuf = torch.full((E + 4,), 7, dtype=torch.uint8, device="cuda")
+            _, rew, dn, _ = env.step(torch.from_numpy(acts).cuda(), dones=dbuf[off:off + E], observe=False)
             np.testing.assert_array_equal(rew.cpu().numpy(), orw)
-            np.testing.assert_array_equal(dn.cpu().numpy(), od.astype(bool))
+            np.testing.assert_array_equal(dn.view(torch.uint8).cpu().numpy(), od.astype(np.uint8))
+            guard = dbuf.cpu().numpy()
+            assert (guard[:off] == 7).all() and (guard[off + E:] == 7).all(), "dones written outside its view"
         b, m, lg = get_state_np(env)
         np.testing.assert_array_equal(b, s.boards)
         np.testing.assert_array_equal(m, s.meta)
