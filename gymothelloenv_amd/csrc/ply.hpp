@@ -42,7 +42,10 @@ constexpr int PLY_ACTIONS = 0, PLY_RANDOM = 1;
 //              square NN-1-a (RayMath below).  Against the whole table (16 bytes
 //              per thread): 262,144 boards 5.79 -> 5.45 us per ply, 1,048,576
 //              13.32 -> 13.12 (profiles/r03/ply/ab_half_table.jsonl)
-constexpr int RAYS_MATH = 2, RAYS_HALF = 3;
+//   RAYS_PAIR  computed, split over a lane pair holding the same board (k_sample_step2):
+//              lane 0 runs the four up directions, lane 1 the four down ones on the
+//              turned board, and the pair ORs the two halves through DPP
+constexpr int RAYS_MATH = 2, RAYS_HALF = 3, RAYS_PAIR = 4;
 #ifndef OTH_PLY_MATH_MAX_E
 #define OTH_PLY_MATH_MAX_E 65536  // single-ply launches of at most this many boards compute their rays
 #endif
@@ -98,14 +101,32 @@ __device__ __forceinline__ uint64_t capped_run(uint64_t ray, uint64_t P, uint64_
 // the board turned by 180 degrees (OneWord::turn180), where they point to
 // higher squares too.  r = rays + a, the table of fill_rays<N, true>.
 template <int N, int RAYS>
-__device__ __forceinline__ uint64_t flips_rays(uint64_t P, uint64_t O, const uint64_t* __restrict__ r, int a) {
+__device__ __forceinline__ uint64_t flips_rays(uint64_t P, uint64_t O, const uint64_t* __restrict__ r, int a,
+                                               int h = 0) {
+    if constexpr (RAYS == RAYS_PAIR) {  // lane h of a pair: up (h = 0) or turned down (h = 1) half
+        const uint32_t s0 = (uint32_t)a & 63u, c0 = s0 % N;
+        const bool dn = h != 0;
+        const uint64_t Pt = OneWord<N>::turn180(P), Ot = OneWord<N>::turn180(O);
+        const uint64_t Pl = dn ? Pt : P, Ol = dn ? Ot : O;
+        uint64_t ray[4];
+        RayMath<N>::up(dn ? N * N - 1 - s0 : s0, dn ? N - 1 - c0 : c0, ray);
+        uint64_t f = 0;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) f |= capped_run(ray[d], Pl, Ol);
+        const uint64_t ft = OneWord<N>::turn180(f);
+        f = dn ? ft : f;
+        const uint32_t lo = (uint32_t)f, hi = (uint32_t)(f >> 32);  // the partner's half: quad_perm [1,0,3,2]
+        const uint32_t plo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0xB1, 0xF, 0xF, false);
+        const uint32_t phi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0xB1, 0xF, 0xF, false);
+        return f | ((uint64_t)phi << 32 | plo);
+    }
     uint64_t ray[8];
     if constexpr (RAYS == RAYS_MATH) {  // the turned rays are the up rays of square NN-1-a, column N-1-c
         const uint32_t s = (uint32_t)a & 63u, c = s % N;
         RayMath<N>::up(s, c, ray);
         RayMath<N>::up(N * N - 1 - s, N - 1 - c, ray + 4);
     } else {
-        static_assert(RAYS == RAYS_HALF, "ray source");
+        static_assert(RAYS == RAYS_HALF || RAYS == RAYS_PAIR, "ray source");  // (PAIR returned above)
         const uint64_t* rt = r - (a & 63) + ((N * N - 1 - (a & 63)) & 63);  // (in the table for any a)
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
@@ -131,13 +152,13 @@ __device__ __forceinline__ uint64_t flips_rays(uint64_t P, uint64_t O, const uin
 template <int N, int RAYS = RAYS_MATH>
 __device__ __forceinline__ void step1(uint64_t& B, uint64_t& Wt, uint64_t& L, uint32_t& m, int a, bool valid,
                                       uint32_t flags, const uint64_t* __restrict__ rays, int& reward, int& done,
-                                      int& winner) {
+                                      int& winner, int h = 0) {
     constexpr uint64_t BD = Geo<N>::BOARD.w[0];
     constexpr int NN = N * N;
     const bool tw = (m & M_TURN_WHITE) != 0;
     uint64_t P = tw ? Wt : B, O = tw ? B : Wt;
     const uint64_t mv = valid ? 1ull << a : 0ull;                          // update_board (:391-410)
-    const uint64_t f = flips_rays<N, RAYS>(P, O, rays + (a & 63), a) & (0ull - (uint64_t)valid);
+    const uint64_t f = flips_rays<N, RAYS>(P, O, rays + (a & 63), a, h) & (0ull - (uint64_t)valid);
     P |= f | mv;
     O &= ~f;
     const bool full = (P | O) == BD;                                        // :425-426
