@@ -30,8 +30,6 @@ PLAY_SIZES = list(range(4, 12))  # k_play_rand (one-word boards) and k_play_rand
 # play_rand_n.hip: the max-ILP machine scheduler (one wave per SIMD: latency hidden by the schedule
 # counts, occupancy does not); the rest of the library keeps the default scheduler
 PLAY_FLAGS = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
-if os.environ.get("OTH_PLAY_FLAGS") is not None:  # A/B variants of the tools only (the hash records the flags)
-    PLAY_FLAGS = os.environ["OTH_PLAY_FLAGS"].split()
 DEPS = [os.path.join(CSRC, f) for f in SOURCES] + [os.path.join(ROOT, "include", "othello_mi355x.h")]
 OUT = os.path.join(HERE, "liboth_mi355x.so")
 OBJDIR = os.path.join(HERE, "_objs")
@@ -41,7 +39,15 @@ BASE_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-pass-failed"]
 _HASH_RE = re.compile(rb"oth-src-sha256:([0-9a-f]{64})")
 
 
-def source_hash(extra_flags=()):
+def play_flags(out=OUT):
+    """play_rand_n.hip's scheduler flags: PLAY_FLAGS for the shipped library;
+    OTH_PLAY_FLAGS replaces them for the tools' A/B variants (out != OUT) only."""
+    if out != OUT and os.environ.get("OTH_PLAY_FLAGS") is not None:
+        return os.environ["OTH_PLAY_FLAGS"].split()
+    return list(PLAY_FLAGS)
+
+
+def source_hash(extra_flags=(), out=OUT):
     """SHA-256 over the library's sources (name + bytes) and its build flags."""
     h = hashlib.sha256()
     for p in DEPS:
@@ -49,7 +55,7 @@ def source_hash(extra_flags=()):
         with open(p, "rb") as f:
             h.update(f.read())
         h.update(b"\0")
-    h.update(" ".join([ARCH] + BASE_FLAGS + PLAY_FLAGS + list(extra_flags)).encode())
+    h.update(" ".join([ARCH] + BASE_FLAGS + play_flags(out) + list(extra_flags)).encode())
     return h.hexdigest()
 
 
@@ -64,7 +70,7 @@ def embedded_hash(path=OUT):
 
 
 def needs_build(out=OUT, extra_flags=()):
-    return embedded_hash(out) != source_hash(extra_flags)
+    return embedded_hash(out) != source_hash(extra_flags, out)
 
 
 def _jobs():
@@ -80,7 +86,7 @@ def build(force=False, verbose=True, extra_flags=(), out=OUT, jobs=None, only_si
     if not force and not needs_build(out, extra_flags):
         return out
     assert only_sizes is None or out != OUT, "the shipped library is always built whole"
-    digest = source_hash(extra_flags)
+    digest = source_hash(extra_flags, out)
     objdir = OBJDIR if out == OUT else os.path.join(OBJDIR, os.path.splitext(os.path.basename(out))[0])
     shutil.rmtree(objdir, ignore_errors=True)
     os.makedirs(objdir)
@@ -90,7 +96,7 @@ def build(force=False, verbose=True, extra_flags=(), out=OUT, jobs=None, only_si
     units += [(os.path.join(CSRC, "kernels_n.hip"), os.path.join(objdir, "kernels_n%d.o" % n), ["-DOTH_N=%d" % n])
               for n in SIZES]
     units += [(os.path.join(CSRC, "play_rand_n.hip"), os.path.join(objdir, "play_rand_n%d.o" % n),
-               ["-DOTH_N=%d" % n] + PLAY_FLAGS) for n in PLAY_SIZES]
+               ["-DOTH_N=%d" % n] + play_flags(out)) for n in PLAY_SIZES]
 
     def compile_one(u):
         src, obj, defs = u
@@ -111,6 +117,9 @@ def build(force=False, verbose=True, extra_flags=(), out=OUT, jobs=None, only_si
         missing = [o for o in reuse if not os.path.exists(o)]
         if missing:
             raise RuntimeError("only_sizes needs the main build's objects: %s" % missing[:3])
+        if embedded_hash(OUT) != source_hash():  # the reused objects must come from these sources
+            raise RuntimeError("only_sizes reuses the main build's objects: rebuild %s from the current sources "
+                               "first" % OUT)
     with concurrent.futures.ThreadPoolExecutor(jobs or _jobs()) as ex:
         objs = list(ex.map(compile_one, units)) + reuse
     subprocess.check_call([HIPCC, "--offload-arch=%s" % ARCH, "-shared", "-o", out + ".tmp"] + objs, cwd=ROOT)

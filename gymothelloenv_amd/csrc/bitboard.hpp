@@ -237,7 +237,7 @@ OTH_HD U2 and_or(U2 a, U2 b, U2 c) {
     return (a & b) | c;
 }
 
-// plain 64-bit words with U2's interface (OneWord::greedy runs on either)
+// constant shift of a plain 64-bit word (OneWord::greedy's run lengths)
 template <int S>
 OTH_HD uint64_t sh(uint64_t x) {
     static_assert(S > -64 && S < 64, "shift within one word");
@@ -245,23 +245,7 @@ OTH_HD uint64_t sh(uint64_t x) {
     else return x >> -S;
 }
 OTH_HD bool any(uint64_t a) { return a != 0ull; }
-template <typename V>
-OTH_HD V from64(uint64_t v) {
-    if constexpr (std::is_same<V, U2>::value) return u2(v);
-    else return v;
-}
-template <typename V>
-OTH_HD uint64_t to64(V v) {
-    if constexpr (std::is_same<V, U2>::value) return u64(v);
-    else return v;
-}
 
-#ifndef OTH_GREEDY_WORD64
-#define OTH_GREEDY_WORD64 1  // OneWord::greedy on uint64_t (1); dword pairs (0) miscompile inside k_play on gfx950, see DESIGN.md
-#endif
-#ifndef OTH_GREEDY_BITOP3
-#define OTH_GREEDY_BITOP3 1  // greedy plane adders as explicit 3-input v_bitop3_b32 (xor3 / majority) per dword
-#endif
 // a ^ b ^ c and majority(a, b, c): symmetric, so the builtin's operand order does not matter
 OTH_HD uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -336,10 +320,6 @@ struct Geo {
     }
 };
 
-#ifndef OTH_PROP_REUSE
-#define OTH_PROP_REUSE 1  // last doubling step reuses the previous propagator where it covers N - 2
-#endif
-
 // (a & b) | c (the multi-word Kogge-Stone step; one-word and dword scans use U2 / DW)
 template <int W>
 OTH_HD BB<W> and_or(const BB<W>& a, const BB<W>& b, const BB<W>& c) {
@@ -355,8 +335,8 @@ struct Pro {
     static constexpr int S = DR * N + DC;
     static constexpr int STEPS = Geo<N>::MAXRUN > 8 ? 4 : (Geo<N>::MAXRUN > 4 ? 3 : (Geo<N>::MAXRUN > 2 ? 2 : 1));
     // the last step reuses the previous propagator when that covers N - 2 (see legal_axis)
-    static constexpr bool R3 = OTH_PROP_REUSE && STEPS == 3 && Geo<N>::MAXRUN <= 6;
-    static constexpr bool R4 = OTH_PROP_REUSE && STEPS == 4 && Geo<N>::MAXRUN <= 12;
+    static constexpr bool R3 = STEPS == 3 && Geo<N>::MAXRUN <= 6;
+    static constexpr bool R4 = STEPS == 4 && Geo<N>::MAXRUN <= 12;
     BB<W> p1, p2, p4, p8;
     OTH_HD explicit Pro(const BB<W>& O) {
         p1 = O & Geo<N>::template dst_mask<DC>();
@@ -383,20 +363,6 @@ struct Pro {
     OTH_HD BB<W> run_from(const BB<W>& g) const { return fill(shift<W, S>(g) & p1); }
 };
 
-// Legal squares for the mover P along one direction, or-ed into L (unmasked
-// by emptiness; legal_moves applies that once).
-template <int N, int DR, int DC>
-OTH_HD void legal_dir(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O, BB<Geo<N>::W>& L) {
-    constexpr int W = Geo<N>::W;
-    const Pro<N, DR, DC> pro(O);
-    const BB<W> t = pro.run_from(P);
-    L = and_or(shift<W, DR * N + DC>(t), Geo<N>::template dst_mask<DC>(), L);
-}
-
-#ifndef OTH_AXIS_LEGAL
-#define OTH_AXIS_LEGAL 1
-#endif
-
 // Both directions of one axis (shift S > 0 and -S) for the mover P against the
 // propagator p1 (opponent discs that a run may pass through).  For the
 // horizontal and diagonal axes p1 excludes the two edge columns: a run can
@@ -412,8 +378,8 @@ OTH_HD void legal_axis(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& p1, BB<Geo<N
     // The last doubling step may reuse the previous propagator when that still
     // covers the longest run: 1 + 1 + 2 + 2 = 6 >= N - 2 for N <= 8, and
     // 1 + 1 + 2 + 4 + 4 = 12 >= N - 2 for N <= 14 (one propagator fewer per axis).
-    constexpr bool R3 = OTH_PROP_REUSE && STEPS == 3 && Geo<N>::MAXRUN <= 6;
-    constexpr bool R4 = OTH_PROP_REUSE && STEPS == 4 && Geo<N>::MAXRUN <= 12;
+    constexpr bool R3 = STEPS == 3 && Geo<N>::MAXRUN <= 6;
+    constexpr bool R4 = STEPS == 4 && Geo<N>::MAXRUN <= 12;
     BB<W> p2, p4, p8;
     if constexpr (STEPS > 1) p2 = p1 & shift<W, S>(p1);
     if constexpr (STEPS > 2 && !R3) p4 = p2 & shift<W, 2 * S>(p2);
@@ -467,38 +433,23 @@ OTH_HD void legal_axis(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& p1, BB<Geo<N
 // which some direction holds >= 1 opponent disc followed by an own disc.
 // Written as rays cast FROM the mover's discs; the set of (square, direction)
 // pairs it accepts is the same as the reference's per-cell scan.
-#ifndef OTH_DW_SCAN
-#define OTH_DW_SCAN 4  // multi-word boards of up to this many words: legal_moves_fills on dwords (legal_moves_fills_dw)
-#endif
-#ifndef OTH_DW_LEGAL
-#define OTH_DW_LEGAL 1  // legal_moves (Solo: k_step, k_sample_step, k_step_vs, ...) on dwords too for multi-word boards
-#endif
+// Multi-word boards (W = 2..4) scan on dwords (legal_moves_fills_dw), both
+// here and in legal_moves_fills.
 template <int N>
 OTH_HD BB<Geo<N>::W> legal_moves_fills_dw(const BB<Geo<N>::W>& Pb, const BB<Geo<N>::W>& Ob, BB<Geo<N>::W> t[8]);
 
 template <int N>
 OTH_HD BB<Geo<N>::W> legal_moves(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O) {
-    if constexpr (Geo<N>::W >= 2 && Geo<N>::W <= OTH_DW_SCAN && OTH_DW_LEGAL) {
+    if constexpr (Geo<N>::W >= 2) {
         BB<Geo<N>::W> t[8];  // the fills are dead here
         return legal_moves_fills_dw<N>(P, O, t);
     }
     auto L = zero<Geo<N>::W>();
-#if OTH_AXIS_LEGAL
     const auto pin = O & Geo<N>::INNER;
     legal_axis<N, 1>(P, pin, L);      // E / W
     legal_axis<N, N>(P, O, L);        // S / N
     legal_axis<N, N + 1>(P, pin, L);  // SE / NW
     legal_axis<N, N - 1>(P, pin, L);  // SW / NE
-#else
-    legal_dir<N, 0, 1>(P, O, L);
-    legal_dir<N, 0, -1>(P, O, L);
-    legal_dir<N, 1, 0>(P, O, L);
-    legal_dir<N, -1, 0>(P, O, L);
-    legal_dir<N, 1, 1>(P, O, L);
-    legal_dir<N, 1, -1>(P, O, L);
-    legal_dir<N, -1, 1>(P, O, L);
-    legal_dir<N, -1, -1>(P, O, L);
-#endif
     return L & ~(P | O) & Geo<N>::BOARD;
 }
 
@@ -509,7 +460,7 @@ OTH_HD BB<Geo<N>::W> legal_moves(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O)
 // direction -S and vice versa.
 template <int N>
 OTH_HD BB<Geo<N>::W> legal_moves_fills(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O, BB<Geo<N>::W> t[8]) {
-    if constexpr (Geo<N>::W >= 2 && Geo<N>::W <= OTH_DW_SCAN) return legal_moves_fills_dw<N>(P, O, t);
+    if constexpr (Geo<N>::W >= 2) return legal_moves_fills_dw<N>(P, O, t);
     auto L = zero<Geo<N>::W>();
     const auto pin = O & Geo<N>::INNER;
     legal_axis<N, 1>(P, pin, L, t[4], t[0]);      // W / E
@@ -604,8 +555,8 @@ OTH_HD DW<K> sh(const DW<K>& x) {
 template <int N, int S, int K = 2 * Geo<N>::W>
 OTH_HD void legal_axis_dw(const DW<K>& P, const DW<K>& p1, DW<K>& L, DW<K>& tplus, DW<K>& tminus) {
     constexpr int STEPS = Pro<N, 0, 1>::STEPS;
-    constexpr bool R3 = OTH_PROP_REUSE && STEPS == 3 && Geo<N>::MAXRUN <= 6;
-    constexpr bool R4 = OTH_PROP_REUSE && STEPS == 4 && Geo<N>::MAXRUN <= 12;
+    constexpr bool R3 = STEPS == 3 && Geo<N>::MAXRUN <= 6;
+    constexpr bool R4 = STEPS == 4 && Geo<N>::MAXRUN <= 12;
     DW<K> p2{}, p4{}, p8{};
     if constexpr (STEPS > 1) p2 = p1 & sh<S>(p1);
     if constexpr (STEPS > 2 && !R3) p4 = p2 & sh<2 * S>(p2);
@@ -862,9 +813,6 @@ OTH_HD BB<Geo<N>::W> flips(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O, const
 // t[d] = the fill of ray direction d: opponent discs from which an own disc is
 // reached going along d through opponent discs only.  The run a move on square
 // a flips along d is the contiguous part of ray d from a inside t[d].
-#ifndef OTH_CARRY_H
-#define OTH_CARRY_H 1  // OneWord: the horizontal axis of the legal scan by carry chains (axis_h)
-#endif
 
 template <int N>
 struct OneWord {
@@ -900,7 +848,7 @@ struct OneWord {
     // a row, reversed), an involution on the board's NN bits.
     static OTH_HD uint64_t turn180(uint64_t x) { return rev64(x) >> (64 - N * N); }
 
-    // The horizontal axis by carries (OTH_CARRY_H): stepping +1 from an own
+    // The horizontal axis by carries: stepping +1 from an own
     // disc through a run of opponent discs of the inner columns is a carry
     // chain of (P << 1) + pin, which clears the run and sets the square past
     // it, so the fill is pin & ~((P << 1) + pin) -- one v_lshl_add_u64 and an
@@ -921,11 +869,7 @@ struct OneWord {
     static OTH_HD uint64_t legal(uint64_t Pw, uint64_t Ow, uint64_t t[8]) {
         const U2 P = u2(Pw), O = u2(Ow), pin = O & u2(IN);
         U2 L{0u, 0u}, f[8];
-#if OTH_CARRY_H
         axis_h(Pw, Ow & IN, L, f[4], f[0]);
-#else
-        axis<1>(P, pin, L, f[4], f[0]);
-#endif
         axis<N>(P, O, L, f[5], f[1]);
         axis<N + 1>(P, pin, L, f[6], f[2]);
         axis<N - 1>(P, pin, L, f[7], f[3]);
@@ -939,43 +883,34 @@ struct OneWord {
     // from doubling shifts; the nested A_1..A_6 count in binary as
     // (A1^..^A6, (A2^A4)|A6, A4).  No wrap-around masks: the horizontal and
     // diagonal fills hold no edge-column square, and every A_j lies in A_1.
-    template <int S, typename V>
-    static OTH_HD void run_len(V T, V out[3]) {
+    template <int S>
+    static OTH_HD void run_len(uint64_t T, uint64_t out[3]) {
         constexpr int R = N - 2;
-        const V z = from64<V>(0ull);
-        const V A1 = sh<-S>(T);
-        V A2 = z, A3 = z, A4 = z, A5 = z, A6 = z;
+        const uint64_t A1 = sh<-S>(T);
+        uint64_t A2 = 0, A3 = 0, A4 = 0, A5 = 0, A6 = 0;
         if constexpr (R >= 2) A2 = A1 & sh<-S>(A1);
         if constexpr (R >= 3) A3 = A2 & sh<-2 * S>(A1);
         if constexpr (R >= 4) A4 = A2 & sh<-2 * S>(A2);
         if constexpr (R >= 5) A5 = A4 & sh<-4 * S>(A1);
         if constexpr (R >= 6) A6 = A4 & sh<-4 * S>(A2);
-        if constexpr (std::is_same<V, uint64_t>::value && OTH_GREEDY_BITOP3)
-            out[0] = xor3_64(xor3_64(A1, A2, A3), A4, A5) ^ A6;
-        else
-            out[0] = A1 ^ A2 ^ A3 ^ A4 ^ A5 ^ A6;
+        out[0] = xor3_64(xor3_64(A1, A2, A3), A4, A5) ^ A6;
         out[1] = (A2 ^ A4) | A6;
         out[2] = A4;
     }
-    // out[0..NO) = a[0..NA) + b[0..NB) on bit planes (ripple carry, carries past NO dropped)
-    template <int NA, int NB, int NO, typename V>
-    static OTH_HD void add_planes(const V* a, const V* b, V* out) {
-        const V z = from64<V>(0ull);
-        V c = z;
+    // out[0..NO) = a[0..NA) + b[0..NB) on bit planes (ripple carry, carries past NO
+    // dropped): a half adder, then one 3-input op per dword for each sum and carry
+    template <int NA, int NB, int NO>
+    static OTH_HD void add_planes(const uint64_t* a, const uint64_t* b, uint64_t* out) {
+        uint64_t c = 0;
 #pragma unroll
         for (int i = 0; i < NO; ++i) {
-            const V x = i < NA ? a[i] : z, y = i < NB ? b[i] : z;
-            if constexpr (std::is_same<V, uint64_t>::value && OTH_GREEDY_BITOP3) {
-                if (i == 0) {  // half adder: no carry in
-                    out[i] = x ^ y;
-                    c = x & y;
-                } else {  // full adder: one 3-input op per dword for the sum and one for the carry
-                    out[i] = xor3_64(x, y, c);
-                    c = maj3_64(x, y, c);
-                }
+            const uint64_t x = i < NA ? a[i] : 0ull, y = i < NB ? b[i] : 0ull;
+            if (i == 0) {
+                out[i] = x ^ y;
+                c = x & y;
             } else {
-                out[i] = x ^ y ^ c;
-                c = (x & y) | (c & (x | y));
+                out[i] = xor3_64(x, y, c);
+                c = maj3_64(x, y, c);
             }
         }
     }
@@ -984,18 +919,20 @@ struct OneWord {
     // (np.argmax); -1 without candidates.  The eight run lengths are summed on
     // bit planes (at most 19 flips on a board of N <= 8: 5 planes), then the
     // largest total among the candidates is found plane by plane from the top.
+    // The planes are plain 64-bit words: on dword pairs (U2) the gfx950 backend
+    // miscompiled them inside k_play ("A compiler hazard";
+    // tests/test_gpu_hazards.py pins the position).
     static OTH_HD int greedy(const uint64_t t[8], uint64_t legal) {
-        using V = typename std::conditional<OTH_GREEDY_WORD64 != 0, uint64_t, U2>::type;
-        V n[8][3];
-        run_len<1>(from64<V>(t[0]), n[0]);
-        run_len<N>(from64<V>(t[1]), n[1]);
-        run_len<N + 1>(from64<V>(t[2]), n[2]);
-        run_len<N - 1>(from64<V>(t[3]), n[3]);
-        run_len<-1>(from64<V>(t[4]), n[4]);
-        run_len<-N>(from64<V>(t[5]), n[5]);
-        run_len<-N - 1>(from64<V>(t[6]), n[6]);
-        run_len<-N + 1>(from64<V>(t[7]), n[7]);
-        V s4[4][4], s5[2][5], tot[5];
+        uint64_t n[8][3];
+        run_len<1>(t[0], n[0]);
+        run_len<N>(t[1], n[1]);
+        run_len<N + 1>(t[2], n[2]);
+        run_len<N - 1>(t[3], n[3]);
+        run_len<-1>(t[4], n[4]);
+        run_len<-N>(t[5], n[5]);
+        run_len<-N - 1>(t[6], n[6]);
+        run_len<-N + 1>(t[7], n[7]);
+        uint64_t s4[4][4], s5[2][5], tot[5];
 #pragma unroll
         for (int i = 0; i < 4; ++i) add_planes<3, 3, 4>(n[2 * i], n[2 * i + 1], s4[i]);
         add_planes<4, 4, 5>(s4[0], s4[1], s5[0]);
@@ -1004,16 +941,12 @@ struct OneWord {
         uint64_t cand = legal;
 #pragma unroll
         for (int i = 4; i >= 0; --i) {
-            const uint64_t h = cand & to64(tot[i]);
+            const uint64_t h = cand & tot[i];
             cand = h ? h : cand;
         }
         return cand ? __builtin_ctzll(cand) : -1;
     }
 };
-
-#ifndef OTH_SELECT
-#define OTH_SELECT 2  // 1: six-level binary search; 2: byte prefix counts compared in parallel + nibble table
-#endif
 
 // Position of the j-th set bit (j < popcount) of every 4-bit value v, 2 bits
 // per (v, j) at bit offset 2 * (4 v + j): two 64-bit constants.
@@ -1031,7 +964,6 @@ constexpr uint64_t sel4_table(int half) {
 }
 
 // Index of the k-th (0-based, ascending) set bit of a non-zero word, k < popcount.
-#if OTH_SELECT == 2
 // Shallow form for one wave per SIMD: the 32-bit half by the low word's count,
 // the byte by comparing k with the three byte-prefix counts at once, the nibble
 // by one count, the bit from a 128-bit table.
@@ -1086,34 +1018,6 @@ OTH_HD int select64_tab(uint64_t x, int k, const uint8_t* sel8) {
 #endif
     return (up ? 32 : 0) + 8 * b + sel8[8 * byte + (uint32_t)(kk - qb)];
 }
-#else
-OTH_HD int select64(uint64_t x, int k) {
-    int pos = 0;
-    uint32_t lo = (uint32_t)x;
-    int c = popc64(lo);
-    uint32_t v = lo;
-    if (k >= c) {
-        k -= c;
-        v = (uint32_t)(x >> 32);
-        pos = 32;
-    }
-#pragma unroll
-    for (int width = 16; width >= 1; width >>= 1) {
-        uint32_t low = v & ((1u << width) - 1u);
-        int cl = popc64(low);
-        if (k >= cl) {
-            k -= cl;
-            v >>= width;
-            pos += width;
-        } else {
-            v = low;
-        }
-    }
-    return pos;
-}
-#endif
-
-#if OTH_SELECT == 2
 // select_bit with select64_tab inside the word (k < popcount: a pick from a non-empty mask)
 template <int W>
 OTH_HD int select_bit_tab(const BB<W>& b, int k, const uint8_t* sel8) {
@@ -1130,7 +1034,6 @@ OTH_HD int select_bit_tab(const BB<W>& b, int k, const uint8_t* sel8) {
     }
     return res;
 }
-#endif
 template <int W>
 OTH_HD int select_bit(const BB<W>& b, int k) {
     if constexpr (W == 1) {  // branch-free: -1 when k >= popcount (no legal move)
@@ -1157,16 +1060,14 @@ OTH_HD int select_bit(const BB<W>& b, int k) {
 struct U4 {
     uint32_t x, y, z, w;
 };
-#ifndef OTH_PHILOX_XOR3
-#define OTH_PHILOX_XOR3 1  // Philox rounds >= 2: each a ^ b ^ k as one v_bitop3_b32 (the backend emits two v_xor_b32)
-#endif
-// a ^ b ^ c; round r of philox4 takes the 3-input form only from round 2 on,
+// a ^ b ^ c; round r of philox4 takes the 3-input form (one v_bitop3_b32; the
+// backend emits two v_xor_b32) only from round 2 on,
 // where every operand but the key varies per lane (rounds 0 and 1 keep their
 // uniform parts on the scalar unit)
 template <int R>
 OTH_HD uint32_t philox_xor(uint32_t a, uint32_t b, uint32_t c) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    if constexpr (OTH_PHILOX_XOR3 && R >= 2) return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+    if constexpr (R >= 2) return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 #endif
     return a ^ b ^ c;
 }

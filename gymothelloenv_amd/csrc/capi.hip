@@ -434,14 +434,8 @@ int oth_counts(oth_env* env, int64_t* out, int32_t reset, oth_stream_t stream) {
     OTH_CHECK_ENV(env);
     if (!out) return fail(OTH_EINVAL, "out is NULL");
     hipStream_t s = (hipStream_t)stream;
-#if OTH_TALLY_SLOTS
     hipLaunchKernelGGL(k_reduce_wdl, dim3(1), dim3(256), 0, s, env->wdl, env->nslots, out, reset ? 1 : 0);
     return after_launch("oth_counts");
-#else
-    OTH_HIP(hipMemcpyAsync(out, env->wdl, 3 * sizeof(int64_t), hipMemcpyDefault, s));
-    if (reset) OTH_HIP(hipMemsetAsync(env->wdl, 0, 4 * sizeof(unsigned long long), s));
-    return OTH_OK;
-#endif
 }
 
 int oth_counts_vs(oth_env* env, int64_t* out, int32_t reset, oth_stream_t stream) {

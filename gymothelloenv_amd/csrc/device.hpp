@@ -30,83 +30,14 @@
 
 using namespace oth;
 
-#ifndef OTH_FILLS
-#define OTH_FILLS 1  // Fills engine (ray tables + the legal scan's fills) for random play, N <= 8
-#endif
-#ifndef OTH_FILLS_GREEDY
-#define OTH_FILLS_GREEDY 1  // the Fills engine for greedy play too (0: Kogge-Stone flips)
-#endif
-#ifndef OTH_RAYS
-#define OTH_RAYS 1  // LDS ray-table flips for N <= 8 in k_play
-#endif
-#ifndef OTH_REC_TEMPLATE
-#define OTH_REC_TEMPLATE 1  // k_play specialised for "all per-ply outputs stored" (random / greedy)
-#endif
 #ifndef OTH_BLOCK
 #define OTH_BLOCK 256
 #endif
-#ifndef OTH_U32
-#define OTH_U32 1  // Fills engine scans on dword pairs (bitboard.hpp U2)
-#endif
-#ifndef OTH_SOLO_U32
-#define OTH_SOLO_U32 1  // Solo engine (k_step, k_step_vs, ...) scans on dword pairs too for N <= 8
-#endif
-#ifndef OTH_TALLY_ATOMIC
-#define OTH_TALLY_ATOMIC 1  // per-block W/D/L slots updated by posted atomics instead of a read-modify-write
-#endif
-#ifndef OTH_MAXIMIN_PLANES
-#define OTH_MAXIMIN_PLANES 1  // MaxiMin's last search level as the greedy planes' maximum flip count
-#endif
-#ifndef OTH_GREEDY_PLANES_W
-#define OTH_GREEDY_PLANES_W 1  // GreedyPolicy on bit planes for multi-word boards too (bitboard.hpp PlanesW)
-#endif
-#ifndef OTH_GREEDY_PLANES
-#define OTH_GREEDY_PLANES 1  // GreedyPolicy on bit planes for N <= 8 (bitboard.hpp OneWord::greedy)
-#endif
-#ifndef OTH_FILLS_W
-#define OTH_FILLS_W 1  // FillsW engine (ray tables + fills) for multi-word boards
-#endif
-#ifndef OTH_FILLS_W_MAXN
-#define OTH_FILLS_W_MAXN 16  // its BB<W> ray table: 8 * N*N * W words of LDS (16x16: 64 KiB; +30 % at 16x16 all the same)
-#endif
-#ifndef OTH_PICKED
-#define OTH_PICKED 1  // k_play: the action is a pick from the legal mask, flips without a validity branch
-#endif
-#ifndef OTH_FLIP_AND3
-#define OTH_FLIP_AND3 1  // Fills::flip toward higher squares as one 3-input AND (v_bitop3_b32) per dword
-#endif
-#ifndef OTH_OPEN_SPLIT
-#define OTH_OPEN_SPLIT 1  // k_play_rand: a copy of the ply loop without random-opening bookkeeping
-#endif
-#ifndef OTH_FAST_GREEDY
-#define OTH_FAST_GREEDY 1  // k_play_rand<N, GREEDY>: the same restructuring for greedy play (N <= 8)
-#endif
-#ifndef OTH_FAST_RANDOM_W
-#define OTH_FAST_RANDOM_W 1  // k_play_rand_w: the same restructured random play for multi-word boards (N >= 9)
-#endif
-#ifndef OTH_OBS_WAVE
-#define OTH_OBS_WAVE 1  // observations: one wave per 64 boards (k_observe_w) instead of one board per wave (k_observe_q)
-#endif
-#ifndef OTH_SS_PAIR
-#define OTH_SS_PAIR 1  // oth_sample_step on lane pairs for one-word boards (k_sample_step2)
-#endif
-#ifndef OTH_SS_QUAD
-#define OTH_SS_QUAD 1  // oth_sample_step on lane quads for one-word boards (k_sample_step4) up to OTH_SS_QUAD_MAX_E
-#endif
 #ifndef OTH_SS_QUAD_MAX_E
-#define OTH_SS_QUAD_MAX_E 16384  // boards: 4 lanes each fill at most 1,024 waves (one per SIMD)
-#endif
-#ifndef OTH_SS2_STAGE
-#define OTH_SS2_STAGE 1  // k_sample_step2 (8x8): the wave's logits rows through LDS, coalesced loads
-#endif
-#ifndef OTH_SS_PAIR_W
-#define OTH_SS_PAIR_W 1  // oth_sample_step on lane pairs for two-word boards too (N = 9..11; Solo step on both lanes)
+#define OTH_SS_QUAD_MAX_E 16384  // oth_sample_step on lane quads up to this many boards: 4 lanes each fill at most 1,024 waves (one per SIMD)
 #endif
 #ifndef OTH_SS_PAIR_W_MAX_E
-#define OTH_SS_PAIR_W_MAX_E 32768  // two-word boards whose rows are not float4-aligned: pairs up to this many boards
-#endif
-#ifndef OTH_FLIP_TURN
-#define OTH_FLIP_TURN 2  // Fills::flip toward lower squares on the board turned by 180 degrees, no 64-bit clz (2: turned rays tabled under the unturned square, +3 % at 8x8; 1: addressed at NN-1-a, -1.5 %)
+#define OTH_SS_PAIR_W_MAX_E 32768  // two-word boards whose rows are not float4-aligned: lane pairs up to this many boards
 #endif
 
 namespace oth_dev {
@@ -245,7 +176,7 @@ __device__ __forceinline__ void store_lane(const Lane<N>& s, uint64_t* __restric
 // ---------------------------------------------------------------------------
 // Engines: who computes legal moves and flips for a lane.
 //   Solo<N>: one lane per board, all 8 directions (any N).
-//   Rays<N>: Solo with LDS ray-table flips (N <= 8).
+//   Fills<N> / FillsW<N>: flips from LDS ray tables and the legal scan's fills.
 //   Quartet<N>: four lanes per board (N <= 8): each lane of the quad scans
 //            one axis and the parts are or-ed through DPP quad_perm steps.
 // ---------------------------------------------------------------------------
@@ -255,14 +186,12 @@ struct Solo {
     static constexpr int RAY_WORDS = 0;
     __device__ __forceinline__ Solo(int, const uint64_t*) {}
     __device__ __forceinline__ BB<Geo<N>::W> legal(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O) const {
-#if OTH_U32 && OTH_SOLO_U32
         if constexpr (Geo<N>::W == 1) {  // the dword-pair scan (fills unused, so dead)
             uint64_t t[8];
             BB<1> r;
             r.w[0] = OneWord<N>::legal(P.w[0], O.w[0], t);
             return r;
         }
-#endif
         return legal_moves<N>(P, O);
     }
     __device__ __forceinline__ BB<Geo<N>::W> flip(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O, int a) const {
@@ -280,7 +209,7 @@ struct Solo {
 
 // TURNED: the tables of the directions toward lower squares (d >= 4) hold
 // their rays on the board turned by 180 degrees (square s -> N*N-1-s), still
-// indexed by the unturned square (Fills with OTH_FLIP_TURN == 2).
+// indexed by the unturned square (Fills).
 template <int N, bool TURNED = false, bool SYNC = true>
 __device__ __forceinline__ void fill_rays(uint64_t* rays) {
     for (int i = threadIdx.x; i < 8 * 64; i += BLOCK) {
@@ -303,46 +232,7 @@ __device__ __forceinline__ void fill_rays(uint64_t* rays) {
     if (SYNC) __syncthreads();
 }
 
-// update_board's flips from one square (othello.py:391-410) with the ray
-// tables: along each ray the run is capped by the NEAREST non-opponent square
-// (lowest set bit of ray & ~O toward higher squares, highest toward lower);
-// the run flips iff that square holds an own disc.  ~20 VALU per direction
-// against ~33 for a Kogge-Stone fill from a single square.
-template <int N>
-struct Rays {
-    static_assert(Geo<N>::W == 1, "ray tables are for one-word boards (N <= 8)");
-    static constexpr int LANES = 1;
-    static constexpr int RAY_WORDS = 8 * 64;
-    const uint64_t* rays;
-    __device__ __forceinline__ Rays(int, const uint64_t* lds) : rays(lds) {}
-    __device__ __forceinline__ BB<1> legal(const BB<1>& P, const BB<1>& O) const { return legal_moves<N>(P, O); }
-    __device__ __forceinline__ BB<1> flip(const BB<1>& Pb, const BB<1>& Ob, int a) const {
-        const uint64_t P = Pb.w[0], nO = ~Ob.w[0];
-        const uint64_t* r = rays + a;
-        uint64_t f = 0;
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {  // toward higher squares
-            const uint64_t ray = r[64 * d];
-            const uint64_t x = ray & nO;
-            const uint64_t fb = x & (0ull - x);
-            f |= (fb & P) ? (ray & (fb - 1ull)) : 0ull;
-        }
-#pragma unroll
-        for (int d = 4; d < 8; ++d) {  // toward lower squares
-            const uint64_t ray = r[64 * d];
-            const uint64_t x = ray & nO;
-            const uint64_t hb = x ? (0x8000000000000000ull >> __clzll(x)) : 0ull;
-            f |= (hb & P) ? (ray & (0ull - (hb << 1))) : 0ull;
-        }
-        BB<1> out;
-        out.w[0] = f;
-        return out;
-    }
-    __device__ __forceinline__ void prime(const Lane<N>&) const {}
-    __device__ __forceinline__ bool leader() const { return true; }
-};
-
-// Fills<N>: Rays whose flips reuse the legal scan.  legal_moves' axis scans
+// Fills<N>: flips from the ray tables and the legal scan's fills.  legal_moves' axis scans
 // compute, for the side to move, the fills t(dir) = opponent discs reachable
 // from an own disc through contiguous opponent discs stepping in direction dir
 // (the scan shifts them once more onto the empty squares).  Kept in registers
@@ -367,54 +257,12 @@ struct Fills {
     mutable uint64_t t[8];
     __device__ __forceinline__ Fills(int, const uint64_t* lds) : rays(lds) {}
 
-    template <int S>
-    __device__ __forceinline__ static void axis(uint64_t P, uint64_t p1, uint64_t& L, uint64_t& tplus,
-                                                uint64_t& tminus) {
-        // runs are at most N - 2 <= 6 long: the third doubling step reuses p2 (1 + 1 + 2 + 2)
-        uint64_t p2 = 0, p4 = 0;
-        if constexpr (STEPS > 1) p2 = p1 & (p1 << S);
-        if constexpr (STEPS > 2 && !OTH_PROP_REUSE) p4 = p2 & (p2 << (2 * S));
-        uint64_t x = (P << S) & p1;
-        x |= p1 & (x << S);
-        if constexpr (STEPS > 1) x |= p2 & (x << (2 * S));
-        if constexpr (STEPS > 2) {
-            if constexpr (OTH_PROP_REUSE) x |= p2 & (x << (2 * S));
-            else x |= p4 & (x << (4 * S));
-        }
-        tplus = x;
-        L |= x << S;
-        const uint64_t p2m = p2 >> S;
-        x = (P >> S) & p1;
-        x |= p1 & (x >> S);
-        if constexpr (STEPS > 1) x |= p2m & (x >> (2 * S));
-        if constexpr (STEPS > 2) {
-            if constexpr (OTH_PROP_REUSE) x |= p2m & (x >> (2 * S));
-            else x |= (p4 >> (3 * S)) & (x >> (4 * S));
-        }
-        tminus = x;
-        L |= x >> S;
-    }
-    // get_possible_actions for mover P (legal_moves' axis-paired scan), keeping the fills
+    // get_possible_actions for mover P, keeping the fills: the axis-paired scan
+    // on dwords (bitboard.hpp OneWord: v_bitop3 / v_and_or, carry-chain horizontal axis)
     __device__ __forceinline__ BB<1> legal(const BB<1>& Pb, const BB<1>& Ob) const {
-        static_assert(Pro<N, 0, 1>::STEPS <= 3, "N <= 8");
-#if OTH_U32
-        // the same scan on dwords (bitboard.hpp OneWord): v_bitop3 / v_and_or
-        // instead of and + or pairs, 32-bit shifts instead of v_lshl*_b64
-        static_assert(OTH_PROP_REUSE, "dword scan assumes the reused last propagator");
         BB<1> r;
         r.w[0] = OneWord<N>::legal(Pb.w[0], Ob.w[0], t);
         return r;
-#else
-        const uint64_t P = Pb.w[0], O = Ob.w[0], pin = O & IN;
-        uint64_t L = 0;
-        axis<1>(P, pin, L, t[4], t[0]);          // W uses +1 fill, E uses -1 fill
-        axis<N>(P, O, L, t[5], t[1]);            // N / S
-        axis<N + 1>(P, pin, L, t[6], t[2]);      // NW / SE
-        axis<N - 1>(P, pin, L, t[7], t[3]);      // NE / SW
-        BB<1> r;
-        r.w[0] = L & ~(P | O) & BD;
-        return r;
-#endif
     }
     __device__ __forceinline__ BB<1> flip(const BB<1>&, const BB<1>&, int a) const {
         const uint64_t* r = rays + a;
@@ -423,40 +271,23 @@ struct Fills {
         for (int d = 0; d < 4; ++d) {  // toward higher squares: cap = lowest ray square outside the fill
             const uint64_t ray = r[64 * d];
             const uint64_t y = ray & ~t[d];
-#if OTH_FLIP_AND3
             // ray & ((y & -y) - 1) == ray & t & (y - 1): one 3-input AND per dword
             f |= and3_64(ray, t[d], y - 1ull);
-#else
-            f |= ray & ((y & (0ull - y)) - 1ull);
-#endif
         }
-#if OTH_FLIP_TURN
         // toward lower squares on the board turned by 180 degrees (square s ->
         // NN-1-s, OneWord::turn180): the ray runs toward higher squares there,
         // so the same lowest-bit form applies to the turned fill; one turn of
-        // the or-ed runs at the end.  OTH_FLIP_TURN 2: the turned rays are
-        // tabled under the unturned square (same address as the other four);
-        // 1: ray d from a is ray d-4 from NN-1-a
-        const uint64_t* rt = OTH_FLIP_TURN == 2 ? r : rays + (N * N - 1 - a) - 4 * 64;
+        // the or-ed runs at the end.  The turned rays are tabled under the
+        // unturned square (the same address as the other four)
         uint64_t g = 0;
 #pragma unroll
         for (int d = 4; d < 8; ++d) {
-            const uint64_t ray = rt[64 * d];
+            const uint64_t ray = r[64 * d];
             const uint64_t tt = OneWord<N>::turn180(t[d]);
             const uint64_t y = ray & ~tt;
             g |= and3_64(ray, tt, y - 1ull);
         }
         f |= OneWord<N>::turn180(g);
-#else
-#pragma unroll
-        for (int d = 4; d < 8; ++d) {  // toward lower squares: cap = highest ray square outside the fill
-            // y == 0 only when the ray is empty (the edge square of a ray is never in a fill)
-            const uint64_t ray = r[64 * d];
-            const uint64_t y = (ray & ~t[d]) | 1ull;
-            const uint64_t hb = 0x8000000000000000ull >> __clzll(y);
-            f |= ray & (0ull - (hb << 1));
-        }
-#endif
         BB<1> out;
         out.w[0] = f;
         return out;
@@ -511,7 +342,7 @@ struct FillsW {
 template <typename Eng>
 struct turned_rays : std::false_type {};
 template <int N>
-struct turned_rays<Fills<N>> : std::integral_constant<bool, OTH_FLIP_TURN == 2> {};
+struct turned_rays<Fills<N>> : std::true_type {};
 
 template <typename Eng>
 struct is_fills_w : std::false_type {};
@@ -704,46 +535,10 @@ __device__ __forceinline__ int random_action(const Lane<N>& s, uint32_t u) {
 
 // GreedyPolicy.get_action (simple_policies.py:69-92): the move that leaves the
 // mover the most discs = the most flips; np.argmax keeps the first (lowest
-// square) of equal counts, so scan ascending and replace only on '>'.
-template <int N, typename Eng>
-__device__ __forceinline__ void greedy_scan(const Lane<N>& s, int parity, int stride, int& best, int& best_cnt,
-                                            const Eng& eng) {
-    constexpr int W = Geo<N>::W;
-    const bool tw = (s.meta & M_TURN_WHITE) != 0;
-    const BB<W> P = pick(tw, s.white, s.black);
-    const BB<W> O = pick(tw, s.black, s.white);
-    best = -1;
-    best_cnt = -1;
-    int idx = 0;  // rank of the candidate among the legal moves
-#pragma unroll
-    for (int i = 0; i < W; ++i) {
-        uint64_t x = s.legal.w[i];
-        while (x) {
-            const int b = __builtin_ctzll(x);
-            x &= x - 1;
-            if (stride == 1 || (idx & 1) == parity) {
-                int c;
-                if constexpr (Eng::RAY_WORDS > 0) {
-                    c = popcount(eng.flip(P, O, 64 * i + b));
-                } else {
-                    BB<W> m = zero<W>();
-                    m.w[i] = 1ull << b;
-                    c = popcount(flips<N>(P, O, m));
-                }
-                if (c > best_cnt) {
-                    best_cnt = c;
-                    best = 64 * i + b;
-                }
-            }
-            ++idx;
-        }
-    }
-}
-
+// square) of equal counts.
 template <int N, typename Eng>
 __device__ __forceinline__ int greedy_action(const Lane<N>& s, const Eng& eng) {
     static_assert(Eng::LANES == 1, "greedy runs one lane per board");
-#if OTH_GREEDY_PLANES
     // every square's flip count on bit planes, no loop over the candidates
     if constexpr (std::is_same<Eng, Fills<N>>::value) {
         return eng.greedy(s.legal);  // the fills of the side to move are carried from the last scan
@@ -752,22 +547,14 @@ __device__ __forceinline__ int greedy_action(const Lane<N>& s, const Eng& eng) {
         uint64_t t[8];
         (void)OneWord<N>::legal(tw ? s.white.w[0] : s.black.w[0], tw ? s.black.w[0] : s.white.w[0], t);
         return OneWord<N>::greedy(t, s.legal.w[0]);
-    }
-#endif
-#if OTH_GREEDY_PLANES_W
-    // multi-word boards: the same planes on BB<W> (bitboard.hpp PlanesW)
-    if constexpr (is_fills_w<Eng>::value) {
+    } else if constexpr (is_fills_w<Eng>::value) {  // multi-word boards: the same planes on BB<W> (PlanesW)
         return PlanesW<N>::greedy(eng.t, s.legal);  // fills carried from the last scan
-    } else if constexpr (Geo<N>::W > 1) {
+    } else {
         const bool tw = (s.meta & M_TURN_WHITE) != 0;
         BB<Geo<N>::W> t[8];
         (void)legal_moves_fills<N>(pick(tw, s.white, s.black), pick(tw, s.black, s.white), t);
         return PlanesW<N>::greedy(t, s.legal);
     }
-#endif
-    int best, cnt;
-    greedy_scan<N>(s, 0, 1, best, cnt, eng);
-    return best;
 }
 
 // MaxiMinPolicy(depth).get_action (simple_policies.py:98-163).  P is the side to
@@ -797,7 +584,7 @@ __device__ int maximin_node(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O, cons
             const BB<W> P2 = P | f | m;
             const BB<W> O2 = O & ~(f | m);
             int v = popcount(MINE ? P2 : O2);
-            if constexpr (LVL + 2 == D && OTH_MAXIMIN_PLANES) {
+            if constexpr (LVL + 2 == D) {
                 // the child is the last level: its value is the mover's best flip
                 // count over its moves (bit planes, no loop): my discs after the
                 // child's move are O2 + flips + 1 when I move there, P2 - flips otherwise
@@ -935,10 +722,6 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return v;
 }
 
-#ifndef OTH_TALLY_SLOTS
-#define OTH_TALLY_SLOTS 1
-#endif
-
 // Add this block's finished games {black wins, draws, white wins} to its own
 // slot wdl[blockIdx.x][0..2].  One slot per block: no atomics, no contention
 // (launches on a stream are ordered, and block b of every launch owns slot b);
@@ -947,7 +730,6 @@ __device__ __forceinline__ void tally(unsigned long long* wdl, uint32_t b, uint3
     b = wave_sum(b);
     d = wave_sum(d);
     w = wave_sum(w);
-#if OTH_TALLY_SLOTS
     __shared__ uint32_t part[BLOCK / 64][3];
     const int wave = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
@@ -966,27 +748,14 @@ __device__ __forceinline__ void tally(unsigned long long* wdl, uint32_t b, uint3
         }
         if (sb | sd | sw) {
             unsigned long long* slot = wdl + 4 * (size_t)blockIdx.x;
-#if OTH_TALLY_ATOMIC
             // only this block touches its slot: uncontended atomics without a
             // return value are posted, so the block does not wait for the slot's
             // read (the read-modify-write cost one memory round trip per launch)
             if (sb) atomicAdd(slot + 0, (unsigned long long)sb);
             if (sd) atomicAdd(slot + 1, (unsigned long long)sd);
             if (sw) atomicAdd(slot + 2, (unsigned long long)sw);
-#else
-            slot[0] += sb;
-            slot[1] += sd;
-            slot[2] += sw;
-#endif
         }
     }
-#else
-    if ((threadIdx.x & 63) == 0 && wdl) {
-        if (b) atomicAdd(wdl + 0, (unsigned long long)b);
-        if (d) atomicAdd(wdl + 1, (unsigned long long)d);
-        if (w) atomicAdd(wdl + 2, (unsigned long long)w);
-    }
-#endif
 }
 
 // A launch's draw context (and the search depth of OTH_POLICY_MAXIMIN_DEEP launches).
@@ -1126,7 +895,7 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
                 } else {
                     a = policy_action<N, POLICY>(s, eng, rng.depth);
                 }
-                step_lane<N, Eng, (bool)OTH_PICKED>(s, a, flags, r, d, win, eng);  // a: a pick from s.legal
+                step_lane<N, Eng, true>(s, a, flags, r, d, win, eng);  // a: a pick from s.legal
                 if (d) {
                     cb += win == BLACK_DISK;
                     cd += win == NO_DISK;
@@ -1180,10 +949,6 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
     tally(wdl, cb, cd, cw);
 }
 
-#ifndef OTH_FAST_RANDOM
-#define OTH_FAST_RANDOM 1  // k_play_rand: the headline random play (N <= 8, auto-reset, all outputs stored)
-#endif
-
 // k_play_rand: oth_step_policy(RANDOM) on one-word boards with auto-reset and
 // every per-ply output stored -- the benchmark configuration -- with the
 // same results as k_play<N, RANDOM, Fills<N>, true>, restructured for one
@@ -1208,12 +973,6 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
 struct NoFill {
     __device__ __forceinline__ void operator()() const {}
 };
-#ifndef OTH_SELECT_LDS
-#define OTH_SELECT_LDS 1  // k_play_rand: the bit inside the byte of the k-th legal square from a 2-KiB LDS table
-#endif
-#ifndef OTH_TALLY_SIGN
-#define OTH_TALLY_SIGN 1  // play_rand_fast tallies (sum of black's signs, games, decided games)
-#endif
 // black wins / draws / white wins from play_rand_fast's (sum of black's signs, games, decided games)
 __device__ __forceinline__ void tally_from_signs(uint32_t s, uint32_t g, uint32_t z, uint32_t& cb, uint32_t& cd,
                                                  uint32_t& cw) {
@@ -1232,15 +991,10 @@ __device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_
                                                const uint8_t* sel8 = nullptr) {
     constexpr uint64_t BD = Geo<N>::BOARD.w[0];
     constexpr int NN = N * N;
-    // the k-th legal square: the nibble step by arithmetic, or the byte's bit from the LDS table
+    // the k-th legal square, the bit inside its byte from the 2-KiB LDS table
     auto pick = [&](uint32_t draw) __attribute__((always_inline)) {
         const int k = scale_index(draw, popc64(L));
-#if OTH_SELECT_LDS
         return select64_tab(L, k, sel8);
-#else
-        (void)sel8;
-        return select64(L, k);
-#endif
     };
     if constexpr (POLICY == OTH_POLICY_RANDOM) {
         a = pick(u);  // RandomPolicy (simple_policies.py:37-41); L != 0
@@ -1286,7 +1040,6 @@ __device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_
         const int sg = min(max(df, -1), 1);  // v_med3_i32: the mover's result
         if (flags & OTH_DISK_REWARD) r = oc == 0 ? NN : df;  // :446-459
         else r = sg;                                           // winner * player_turn
-#if OTH_TALLY_SIGN
         // the tally as (cb, cd, cw) = (sum of black's signs, games, decided games),
         // turned into wins / draws / wins by tally_from_signs: three adds, no selects
         const int m = -(int)(meta & M_TURN_WHITE);  // the mover (the turn is not passed on): 0 black, -1 white
@@ -1294,13 +1047,6 @@ __device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_
         cb += (uint32_t)sb;
         cd += 1u;
         cw += (uint32_t)__mul24(sb, sb);
-#else
-        const bool tw = (meta & M_TURN_WHITE) != 0;  // the side that just moved (the turn is not passed on)
-        const bool mover_wins = pc > oc, opp_wins = pc < oc;
-        cb += tw ? opp_wins : mover_wins;
-        cd += !mover_wins && !opp_wins;
-        cw += tw ? mover_wins : opp_wins;
-#endif
         // auto-reset (othello.py:256-271): black to move from the start position
         M = Start<N>::BLACK.w[0];
         O = Start<N>::WHITE.w[0];
@@ -1325,13 +1071,9 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
     static_assert(Geo<N>::W == 1, "one-word boards");
     ply0 += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
     __shared__ __attribute__((aligned(16))) uint64_t lds_rays[Fills<N>::RAY_WORDS];
-#if OTH_SELECT_LDS
     __shared__ __attribute__((aligned(16))) uint64_t lds_sel[256];
     for (int i = threadIdx.x; i < 256; i += BLOCK) lds_sel[i] = sel8_word((uint32_t)i);
     const uint8_t* sel8 = reinterpret_cast<const uint8_t*>(lds_sel);
-#else
-    const uint8_t* sel8 = nullptr;
-#endif
     fill_rays<N, turned_rays<Fills<N>>::value>(lds_rays);  // (its barrier covers lds_sel)
     const int e = blockIdx.x * BLOCK + threadIdx.x;
     uint32_t cb = 0, cd = 0, cw = 0;
@@ -1356,11 +1098,7 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
         int32_t* act_p = actions + e;
         int32_t* rew_p = rewards + e;
         uint8_t* done_p = dones + e;
-#if OTH_TALLY_SIGN
         uint32_t t0 = 0, t1 = 0, t2 = 0;  // play_rand_fast's tally (tally_from_signs)
-#else
-        uint32_t &t0 = cb, &t1 = cd, &t2 = cw;
-#endif
         auto fast = [&](auto OPENC) __attribute__((always_inline)) {
         constexpr bool OPEN = decltype(OPENC)::value;
         auto ply = [&](int p, uint32_t u, const auto& fill) __attribute__((always_inline)) {
@@ -1415,11 +1153,9 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
         };
         if (!slow) {
             // no opening bookkeeping when no board of the wave can have opening plies
-            if (OTH_OPEN_SPLIT && rng.init_rand == 0 && !__any((mt & 0xff00u) != 0)) fast(std::false_type{});
+            if (rng.init_rand == 0 && !__any((mt & 0xff00u) != 0)) fast(std::false_type{});
             else fast(std::true_type{});
-#if OTH_TALLY_SIGN
             tally_from_signs(t0, t1, t2, cb, cd, cw);
-#endif
             const bool tw = (mt & M_TURN_WHITE) != 0;
             s.white.w[0] = tw ? M : O;
             s.black.w[0] = tw ? O : M;
@@ -1465,12 +1201,7 @@ __device__ __forceinline__ void play_rand_fast_w(BB<Geo<N>::W>& M, BB<Geo<N>::W>
                                                  const FILL& fill = FILL{}) {
     constexpr int W = Geo<N>::W;
     constexpr int NN = N * N;
-#if OTH_SELECT_LDS
     a = select_bit_tab(L, scale_index(u, popcount(L)), sel8);  // RandomPolicy (simple_policies.py:37-41); L != 0
-#else
-    (void)sel8;
-    a = select_bit(L, scale_index(u, popcount(L)));  // RandomPolicy (simple_policies.py:37-41); L != 0
-#endif
     meta -= (meta & 0xff00u) ? (1u << M_RAND_SHIFT) : 0u;
     const BB<W> m = square<W>(a);
     const BB<W> f = eng.flip(M, O, a);  // update_board (othello.py:391-410)
@@ -1496,19 +1227,11 @@ __device__ __forceinline__ void play_rand_fast_w(BB<Geo<N>::W>& M, BB<Geo<N>::W>
         const int sg = min(max(df, -1), 1);  // the mover's result
         if (flags & OTH_DISK_REWARD) r = oc == 0 ? NN : df;  // :446-459
         else r = sg;
-#if OTH_TALLY_SIGN
         const int mw = -(int)(meta & M_TURN_WHITE);  // (cb, cd, cw) as in play_rand_fast
         const int sb = (sg ^ mw) - mw;
         cb += (uint32_t)sb;
         cd += 1u;
         cw += (uint32_t)__mul24(sb, sb);
-#else
-        const bool tw = (meta & M_TURN_WHITE) != 0;
-        const bool mover_wins = pc > oc, opp_wins = pc < oc;
-        cb += tw ? opp_wins : mover_wins;
-        cd += !mover_wins && !opp_wins;
-        cw += tw ? mover_wins : opp_wins;
-#endif
         M = Start<N>::BLACK;  // auto-reset (othello.py:256-271)
         O = Start<N>::WHITE;
         L = eng.legal(M, O);
@@ -1530,13 +1253,9 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand_w(uint64_t* __restrict__ bo
     static_assert(W > 1, "multi-word boards");
     ply0 += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
     __shared__ __attribute__((aligned(16))) uint64_t lds_rays[FillsW<N>::RAY_WORDS];
-#if OTH_SELECT_LDS
     __shared__ __attribute__((aligned(16))) uint64_t lds_sel[256];
     for (int i = threadIdx.x; i < 256; i += BLOCK) lds_sel[i] = sel8_word((uint32_t)i);
     const uint8_t* sel8 = reinterpret_cast<const uint8_t*>(lds_sel);
-#else
-    const uint8_t* sel8 = nullptr;
-#endif
     FillsW<N>::fill(lds_rays);  // (its barrier covers lds_sel)
     const int e = blockIdx.x * BLOCK + threadIdx.x;
     uint32_t cb = 0, cd = 0, cw = 0;
@@ -1558,11 +1277,7 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand_w(uint64_t* __restrict__ bo
         int32_t* act_p = actions + e;
         int32_t* rew_p = rewards + e;
         uint8_t* done_p = dones + e;
-#if OTH_TALLY_SIGN
         uint32_t t0 = 0, t1 = 0, t2 = 0;  // play_rand_fast_w's tally (tally_from_signs)
-#else
-        uint32_t &t0 = cb, &t1 = cd, &t2 = cw;
-#endif
         auto ply = [&](uint64_t g, uint32_t u, const auto& fill) __attribute__((always_inline)) {
             int a, r, d;
             play_rand_fast_w<N>(M, O, L, mt, eng, u, flags, rng, id, g, a, r, d, t0, t1, t2, sel8, fill);
@@ -1623,9 +1338,7 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand_w(uint64_t* __restrict__ bo
                     ++p;
                 }
             }
-#if OTH_TALLY_SIGN
             tally_from_signs(t0, t1, t2, cb, cd, cw);
-#endif
             const bool tw = (mt & M_TURN_WHITE) != 0;
 #pragma unroll
             for (int i = 0; i < W; ++i) {
@@ -1904,13 +1617,8 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const uint64_t* __restrict__ 
     }
 }
 
-// Quad kernel for N*N % 4 == 0 (even N): one thread writes 4 consecutive
-// squares of one plane as one vector store (16 B for f32 / i32, 4 B for i8,
-// 2 x 16 B for the 8-byte types), so a wave writes 64 contiguous quads -- the
-// whole (planes, N, N) block of 1 to 4 boards.  The board words are read by
-// the wave's lanes of one board at once (broadcast loads).  Same values as
-// k_observe: LAYOUT / T are template parameters, so the only index math is
-// division by compile-time constants.
+// A quad of 4 consecutive squares of one plane as one vector store (16 B for
+// f32 / i32, 4 B for i8, 2 x 16 B for the 8-byte types): k_observe_w's unit.
 template <typename T>
 struct Quad {
     T v[4];
@@ -1941,69 +1649,14 @@ __device__ __forceinline__ void put_quad(T* out, uint32_t q, int v0, int v1, int
     }
 }
 
-template <int N, int LAYOUT, typename T>
-__global__ __launch_bounds__(BLOCK) void k_observe_q(const uint64_t* __restrict__ boards,
-                                                     const uint16_t* __restrict__ meta,
-                                                     const uint64_t* __restrict__ legal, uint32_t total_quads,
-                                                     T* __restrict__ out) {
-    constexpr int W = Geo<N>::W;
-    constexpr int NN = N * N;
-    static_assert(NN % 4 == 0, "quads of squares");
-    constexpr uint32_t Q = NN / 4;
-    constexpr uint32_t PLANES = LAYOUT == OTH_OBS_BOARD_LEGAL ? 2 : (LAYOUT == OTH_OBS_MAKE_STATE ? 4 : 1);
-    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < total_quads; i += gridDim.x * BLOCK) {
-        const uint32_t q = i % Q;
-        const uint32_t rest = i / Q;
-        const uint32_t plane = rest % PLANES;
-        const uint32_t e = rest / PLANES;
-        const int a0 = 4 * (int)q, wi = a0 / 64, bi = a0 % 64;  // 4 | 64: a quad never straddles words
-        const uint32_t nb = (uint32_t)(boards[(size_t)e * 2 * W + wi] >> bi) & 0xFu;
-        const uint32_t nw = (uint32_t)(boards[(size_t)e * 2 * W + W + wi] >> bi) & 0xFu;
-        int v[4];
-        if constexpr (LAYOUT == OTH_OBS_ABSOLUTE) {  // othello.py:257
-#pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = (int)((nw >> j) & 1u) - (int)((nb >> j) & 1u);
-        } else if constexpr (LAYOUT == OTH_OBS_MAKE_STATE) {  // util.py:48-74
-            const bool tw = (meta[e] & M_TURN_WHITE) != 0;
-            uint32_t bits = 0;
-            if (plane == 0) {
-                bits = nb;
-            } else if (plane == 1) {
-                bits = nw;
-            } else if (plane == 2) {
-                bits = tw ? 0xFu : 0u;
-            } else {  // util.py:55: the legal plane only when >= 2 moves
-                int cnt = 0;
-#pragma unroll
-                for (int k = 0; k < W; ++k) cnt += popc64(legal[(size_t)e * W + k]);
-                bits = cnt > 1 ? (uint32_t)(legal[(size_t)e * W + wi] >> bi) & 0xFu : 0u;
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = (int)((bits >> j) & 1u);
-        } else {  // othello.py:363-376: mover +1, opponent -1; plane 1 the legal squares
-            if (plane == 0) {
-                const bool tw = (meta[e] & M_TURN_WHITE) != 0;
-                const uint32_t mv = tw ? nw : nb, op = tw ? nb : nw;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) v[j] = (int)((mv >> j) & 1u) - (int)((op >> j) & 1u);
-            } else {
-                const uint32_t nl = (uint32_t)(legal[(size_t)e * W + wi] >> bi) & 0xFu;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) v[j] = (int)((nl >> j) & 1u);
-            }
-        }
-        put_quad<T>(out, i, v[0], v[1], v[2], v[3]);
-    }
-}
-
-// k_observe_w (OTH_OBS_WAVE): the same values as k_observe_q, one wave per 64
+// k_observe_w: the same values as k_observe, one wave per 64
 // consecutive boards.  Each lane loads one board (coalesced), then the wave
 // streams the boards' contiguous output region -- 64 x planes x N*N/4 quads --
 // one 64-quad vector store per step, each lane taking the words of the board
-// its quad belongs to from that board's lane (ds_bpermute).  k_observe_q's
-// waves each wait on their own board loads before one 1-KiB store; here one
-// wave's loads feed 64 boards' stores (make_state f32 at 1,048,576 boards:
-// 2.6 TB/s with k_observe_q against 6.9 for a plain fill).
+// its quad belongs to from that board's lane (ds_bpermute).  One board per
+// wave (round 2's k_observe_q, each wave waiting on its own board's loads
+// before one 1-KiB store) reached 2.6 TB/s for make_state f32 at 1,048,576
+// boards; one wave's loads feeding 64 boards' stores, 5.0 (a plain fill: 6.9).
 template <int N, int LAYOUT, typename T>
 __global__ __launch_bounds__(BLOCK) void k_observe_w(const uint64_t* __restrict__ boards,
                                                      const uint16_t* __restrict__ meta,

@@ -99,19 +99,19 @@ void launch_k_play(int lanes_per_board, oth_env* env, int policy, int n_plies, i
             return;
         }
     }
-    if constexpr (OTH_FAST_RANDOM && POL == OTH_POLICY_RANDOM && std::is_same<Eng, Fills<N>>::value) {
+    if constexpr (POL == OTH_POLICY_RANDOM && std::is_same<Eng, Fills<N>>::value) {
         if (actions && rewards && dones && (env->flags & OTH_AUTO_RESET)) {
             launch_play_rand<N, OTH_POLICY_RANDOM>(env, n_plies, actions, rewards, dones, ply0, st);  // play_rand_n.hip
             return;
         }
     }
-    if constexpr (OTH_FAST_GREEDY && POL == OTH_POLICY_GREEDY && std::is_same<Eng, Fills<N>>::value) {
+    if constexpr (POL == OTH_POLICY_GREEDY && std::is_same<Eng, Fills<N>>::value) {
         if (actions && rewards && dones && (env->flags & OTH_AUTO_RESET)) {
             launch_play_rand<N, OTH_POLICY_GREEDY>(env, n_plies, actions, rewards, dones, ply0, st);  // play_rand_n.hip
             return;
         }
     }
-    if constexpr (OTH_FAST_RANDOM_W && POL == OTH_POLICY_RANDOM && std::is_same<Eng, FillsW<N>>::value) {
+    if constexpr (POL == OTH_POLICY_RANDOM && std::is_same<Eng, FillsW<N>>::value) {
         if (actions && rewards && dones && (env->flags & OTH_AUTO_RESET)) {
             if constexpr (Geo<N>::W == 2)  // the max-ILP unit (play_rand_n.hip): 10x10 +5 %, 12x12 -4 %
                 launch_play_rand<N, OTH_POLICY_RANDOM>(env, n_plies, actions, rewards, dones, ply0, st);
@@ -121,7 +121,7 @@ void launch_k_play(int lanes_per_board, oth_env* env, int policy, int n_plies, i
             return;
         }
     }
-    if constexpr (OTH_REC_TEMPLATE && (POL == OTH_POLICY_RANDOM || POL == OTH_POLICY_GREEDY)) {
+    if constexpr (POL == OTH_POLICY_RANDOM || POL == OTH_POLICY_GREEDY) {
         if (actions && rewards && dones) {
             hipLaunchKernelGGL((k_play<N, POL, Eng, true>), grid, block, 0, st, env->boards, env->meta, env->legal,
                                env->E, env->flags, n_plies, actions, rewards, dones, env->wdl, rng_of(env, policy), ply0);
@@ -137,27 +137,19 @@ int launch_play(oth_env* env, int policy, int n_plies, int32_t* actions, int32_t
                 uint64_t ply0, hipStream_t st) {
     return with_policy(policy, [&](auto PC) {
         constexpr int POL = decltype(PC)::value;
-        if constexpr (Geo<N>::W == 1 && OTH_FILLS &&
-                             (POL == OTH_POLICY_RANDOM || (OTH_FILLS_GREEDY && POL == OTH_POLICY_GREEDY))) {
+        // random and greedy play: the fills engines (flips from the legal scan's
+        // fills and a ray table in LDS; FillsW's BB<W> table of 16x16 boards is 64 KiB);
+        // MaxiMin: Kogge-Stone flips (Solo) inside its search
+        if constexpr (Geo<N>::W == 1 && (POL == OTH_POLICY_RANDOM || POL == OTH_POLICY_GREEDY)) {
             launch_k_play<N, POL, Fills<N>>(1, env, policy, n_plies, actions, rewards, dones, ply0, st);
-        } else if constexpr (Geo<N>::W > 1 && OTH_FILLS_W && N <= OTH_FILLS_W_MAXN &&
-                             (POL == OTH_POLICY_RANDOM || POL == OTH_POLICY_GREEDY)) {
+        } else if constexpr (Geo<N>::W > 1 && (POL == OTH_POLICY_RANDOM || POL == OTH_POLICY_GREEDY)) {
             launch_k_play<N, POL, FillsW<N>>(1, env, policy, n_plies, actions, rewards, dones, ply0, st);
-        } else if constexpr (Geo<N>::W == 1 && OTH_RAYS && POL == OTH_POLICY_RANDOM) {
-            // random play with OTH_FILLS=0: ray-table flips with the capping test
-            // (greedy keeps Kogge-Stone flips there: the ray tables' exposed LDS
-            // latency measured -10 % for greedy without the fills)
-            launch_k_play<N, POL, Rays<N>>(1, env, policy, n_plies, actions, rewards, dones, ply0, st);
         } else {
             launch_k_play<N, POL, Solo<N>>(1, env, policy, n_plies, actions, rewards, dones, ply0, st);
         }
         return after_launch("oth_step_policy");
     });
 }
-
-#ifndef OTH_SS_ONE
-#define OTH_SS_ONE 1  // oth_sample_step: one lane samples one board (oth_ms::sample_lane) for boards of <= 2 words
-#endif
 
 template <int N, int G, bool VEC, bool FULL>
 void launch_ss(oth_env* env, const float* logits, long long ld, const float* uniforms, uint64_t counter, int mode,
@@ -167,7 +159,7 @@ void launch_ss(oth_env* env, const float* logits, long long ld, const float* uni
     // where a quarter of the per-lane instruction stream wins (8x8, E = 3001: 5.67 -> 4.83 us per ply);
     // beyond, the quads' duplicated step work loses to pairs (65,536: 7.02 -> 7.45)
     // (the tally slots oth_create sizes cover the quads' grid: one slot per block)
-    if constexpr (Geo<N>::W == 1 && OTH_SS_QUAD) {
+    if constexpr (Geo<N>::W == 1) {
         if (env->E <= OTH_SS_QUAD_MAX_E && grid_for(4LL * env->E) <= env->nslots) {
             hipLaunchKernelGGL((k_sample_step4<N, VEC, FULL>), dim3(grid_for(4LL * env->E)), dim3(BLOCK), 0, st,
                                env->boards, env->meta, env->legal, env->E, env->flags, logits, ld, uniforms, counter,
@@ -180,8 +172,8 @@ void launch_ss(oth_env* env, const float* logits, long long ld, const float* uni
     // two-word boards (9x9 .. 11x11): pairs for float4-aligned rows (10x10: 11.62 -> 11.42 us at 65,536
     // boards) and up to OTH_SS_PAIR_W_MAX_E boards otherwise (9x9 / 11x11 at 16,384: -14 / -20 %; at
     // 65,536 the pairs' scalar loads lose 9 %); 10x10 at 777 .. 32,768 boards: -20 .. -25 %
-    constexpr bool PAIR1 = Geo<N>::W == 1 && N >= 7 && OTH_SS_PAIR;
-    constexpr bool PAIR2 = Geo<N>::W == 2 && OTH_SS_PAIR_W;
+    constexpr bool PAIR1 = Geo<N>::W == 1 && N >= 7;
+    constexpr bool PAIR2 = Geo<N>::W == 2;
     if constexpr (PAIR1 || PAIR2) {
         if (PAIR1 || VEC || env->E <= OTH_SS_PAIR_W_MAX_E) {
             hipLaunchKernelGGL((k_sample_step2<N, VEC, FULL>), dim3(grid_for(2LL * env->E)), dim3(BLOCK), 0, st,
@@ -190,7 +182,8 @@ void launch_ss(oth_env* env, const float* logits, long long ld, const float* uni
             return;
         }
     }
-    constexpr bool ONE = OTH_SS_ONE && Geo<N>::W <= 2;
+    // one lane samples one board (oth_ms::sample_lane) for boards of <= 2 words
+    constexpr bool ONE = Geo<N>::W <= 2;
     const long long lanes = ONE ? (long long)env->E : ((long long)env->E + G - 1) / G * G;
     hipLaunchKernelGGL((k_sample_step<N, G, VEC, FULL, ONE>), dim3(grid_for(lanes)), dim3(BLOCK), 0, st, env->boards,
                        env->meta, env->legal, env->E, env->flags, logits, ld, uniforms, counter, mode, actions,
@@ -203,7 +196,7 @@ template <int N>
 int launch_sample_step(oth_env* env, const float* logits, long long ld, const float* uniforms, uint64_t counter,
                        int mode, int32_t* actions, float* log_probs, float* entropy, int32_t* rewards, uint8_t* dones,
                        uint64_t ply, hipStream_t st) {
-    constexpr int G = Geo<N>::W <= 2 ? OTH_MS_G : 16;
+    constexpr int G = Geo<N>::W <= 2 ? oth_ms::MS_G : 16;
     const bool vec = ((N * N) % 4 == 0) && (ld % 4 == 0) && (((uintptr_t)logits & 15u) == 0);
     const bool full = (mode & OTH_MASKED_FULL_ENTROPY) != 0;
     const int base = mode & 3;
@@ -261,53 +254,27 @@ int launch_legal_moves(int n, const uint64_t* mover, const uint64_t* opp, uint64
     return after_launch("oth_legal_moves");
 }
 
-#ifndef OTH_OBS_QUADS
-#define OTH_OBS_QUADS 1  // k_observe_q (vector stores of 4 squares) where N*N % 4 == 0
-#endif
-
+// one wave per 64 boards (k_observe_w), vector stores of 4 squares: N*N % 4 == 0
 template <int N, typename T>
-void launch_observe_q(oth_env* env, int layout, uint32_t quads, void* out, hipStream_t st) {
+void launch_observe_w(oth_env* env, int layout, void* out, hipStream_t st) {
     T* o = static_cast<T*>(out);
-    if (OTH_OBS_WAVE) {  // one wave per 64 boards (k_observe_w)
-        const dim3 gw(grid_for(((long long)env->E + 63) / 64 * 64));
-        switch (layout) {
-            case OTH_OBS_BOARD:
-                hipLaunchKernelGGL((k_observe_w<N, OTH_OBS_BOARD, T>), gw, dim3(BLOCK), 0, st, env->boards, env->meta,
-                                   env->legal, env->E, o);
-                break;
-            case OTH_OBS_BOARD_LEGAL:
-                hipLaunchKernelGGL((k_observe_w<N, OTH_OBS_BOARD_LEGAL, T>), gw, dim3(BLOCK), 0, st, env->boards,
-                                   env->meta, env->legal, env->E, o);
-                break;
-            case OTH_OBS_MAKE_STATE:
-                hipLaunchKernelGGL((k_observe_w<N, OTH_OBS_MAKE_STATE, T>), gw, dim3(BLOCK), 0, st, env->boards,
-                                   env->meta, env->legal, env->E, o);
-                break;
-            default:
-                hipLaunchKernelGGL((k_observe_w<N, OTH_OBS_ABSOLUTE, T>), gw, dim3(BLOCK), 0, st, env->boards,
-                                   env->meta, env->legal, env->E, o);
-                break;
-        }
-        return;
-    }
-    int grid = grid_for(quads);
-    if (grid > (1 << 20)) grid = 1 << 20;
+    const dim3 gw(grid_for(((long long)env->E + 63) / 64 * 64));
     switch (layout) {
         case OTH_OBS_BOARD:
-            hipLaunchKernelGGL((k_observe_q<N, OTH_OBS_BOARD, T>), dim3(grid), dim3(BLOCK), 0, st, env->boards,
-                               env->meta, env->legal, quads, o);
+            hipLaunchKernelGGL((k_observe_w<N, OTH_OBS_BOARD, T>), gw, dim3(BLOCK), 0, st, env->boards, env->meta,
+                               env->legal, env->E, o);
             break;
         case OTH_OBS_BOARD_LEGAL:
-            hipLaunchKernelGGL((k_observe_q<N, OTH_OBS_BOARD_LEGAL, T>), dim3(grid), dim3(BLOCK), 0, st, env->boards,
-                               env->meta, env->legal, quads, o);
+            hipLaunchKernelGGL((k_observe_w<N, OTH_OBS_BOARD_LEGAL, T>), gw, dim3(BLOCK), 0, st, env->boards,
+                               env->meta, env->legal, env->E, o);
             break;
         case OTH_OBS_MAKE_STATE:
-            hipLaunchKernelGGL((k_observe_q<N, OTH_OBS_MAKE_STATE, T>), dim3(grid), dim3(BLOCK), 0, st, env->boards,
-                               env->meta, env->legal, quads, o);
+            hipLaunchKernelGGL((k_observe_w<N, OTH_OBS_MAKE_STATE, T>), gw, dim3(BLOCK), 0, st, env->boards,
+                               env->meta, env->legal, env->E, o);
             break;
         default:
-            hipLaunchKernelGGL((k_observe_q<N, OTH_OBS_ABSOLUTE, T>), dim3(grid), dim3(BLOCK), 0, st, env->boards,
-                               env->meta, env->legal, quads, o);
+            hipLaunchKernelGGL((k_observe_w<N, OTH_OBS_ABSOLUTE, T>), gw, dim3(BLOCK), 0, st, env->boards,
+                               env->meta, env->legal, env->E, o);
             break;
     }
 }
@@ -317,17 +284,16 @@ int launch_observe(oth_env* env, int layout, int dtype, void* out, hipStream_t s
     const int planes = layout == OTH_OBS_BOARD_LEGAL ? 2 : (layout == OTH_OBS_MAKE_STATE ? 4 : 1);
     const long long total = (long long)env->E * planes * N * N;
     static const int esize[5] = {1, 4, 8, 4, 8};
-    if constexpr ((N * N) % 4 == 0 && OTH_OBS_QUADS) {
+    if constexpr ((N * N) % 4 == 0) {
         // vector stores need a 4-element-aligned base and 32-bit quad indices
         if (dtype >= OTH_I8 && dtype <= OTH_F64 && (uintptr_t)out % (4 * esize[dtype]) == 0 &&
             total / 4 < (1ll << 31)) {
-            const uint32_t quads = (uint32_t)(total / 4);
             switch (dtype) {
-                case OTH_I8: launch_observe_q<N, int8_t>(env, layout, quads, out, st); break;
-                case OTH_I32: launch_observe_q<N, int32_t>(env, layout, quads, out, st); break;
-                case OTH_I64: launch_observe_q<N, long long>(env, layout, quads, out, st); break;
-                case OTH_F32: launch_observe_q<N, float>(env, layout, quads, out, st); break;
-                default: launch_observe_q<N, double>(env, layout, quads, out, st); break;
+                case OTH_I8: launch_observe_w<N, int8_t>(env, layout, out, st); break;
+                case OTH_I32: launch_observe_w<N, int32_t>(env, layout, out, st); break;
+                case OTH_I64: launch_observe_w<N, long long>(env, layout, out, st); break;
+                case OTH_F32: launch_observe_w<N, float>(env, layout, out, st); break;
+                default: launch_observe_w<N, double>(env, layout, out, st); break;
             }
             return after_launch("oth_observe");
         }

@@ -87,9 +87,9 @@ int launch_masked(int n_board, int E, const float* logits, long long ld, const u
     const bool vec = (NN % 4 == 0) && (ld % 4 == 0) && (((uintptr_t)logits & 15u) == 0);
 #define OTH_MS_ARGS \
     vec, E, st, NN, logits, ld, legal, uniforms, seed, id_base, counter, counter_off, mode, actions, log_probs, entropy
-    switch (CH) {  // OTH_MS_G lanes per board up to 128 squares, 16 beyond (registers)
-        case 1: launch_ch<1, OTH_MS_G, OTH_MS_BPR>(OTH_MS_ARGS); break;
-        case 2: launch_ch<2, OTH_MS_G, 1>(OTH_MS_ARGS); break;
+    switch (CH) {  // MS_G lanes per board up to 128 squares, 16 beyond (registers)
+        case 1: launch_ch<1, oth_ms::MS_G, oth_ms::MS_BPR>(OTH_MS_ARGS); break;
+        case 2: launch_ch<2, oth_ms::MS_G, 1>(OTH_MS_ARGS); break;
         case 3: launch_ch<3, 16, 1>(OTH_MS_ARGS); break;
         default: launch_ch<4, 16, 1>(OTH_MS_ARGS); break;
     }

@@ -15,7 +15,7 @@
 // Floating point (fp32), so parity is to the reference's fixtures and a numpy
 // fp64 restatement within tolerance (tests/test_gpu_masked.py).
 //
-// Layout: G lanes per board (OTH_MS_G up to two 64-square chunks, 16
+// Layout: G lanes per board (MS_G = 4 up to two 64-square chunks, 16
 // beyond); lane l holds blocks of 4 squares 4G*bi + 4l .. +3 (dwordx4 loads
 // when the rows are 16-byte aligned: each load instruction covers 16G
 // contiguous bytes of a board), with the legal bits of the same squares, and
@@ -30,14 +30,10 @@
 #include "bitboard.hpp"
 #include "othello_mi355x.h"
 
-#ifndef OTH_MS_BPR
-#define OTH_MS_BPR 1  // boards per lane group, loads of all of them issued first
-#endif
-#ifndef OTH_MS_G
-#define OTH_MS_G 4  // lanes per board up to 128 squares (16 beyond)
-#endif
-
 namespace oth_ms {
+
+constexpr int MS_G = 4;    // lanes per board up to 128 squares (16 beyond)
+constexpr int MS_BPR = 1;  // boards per lane group of one-chunk boards (loads of all of them issued first)
 
 constexpr int MS_BLOCK = 256;
 constexpr uint32_t RNG_SAMPLE = 3;  // Philox purpose word of the sampler's uniforms
@@ -138,40 +134,22 @@ __device__ __forceinline__ void load_slot(Slot<CH, G>& b, int l, int NN, const f
 
 // x where the square is legal (bit j of the block's nibble), -inf elsewhere:
 // a sign-extended bitfield (v_bfe_i32) and a bitfield select (v_bfi_b32).
-#ifndef OTH_MS_BFI
-#define OTH_MS_BFI 1
-#endif
 __device__ __forceinline__ float legal_or_ninf(uint32_t nib, int j, float x) {
-#if OTH_MS_BFI
     const uint32_t mk = (uint32_t)__builtin_amdgcn_sbfe((int)nib, j, 1);  // all ones when legal
     return __uint_as_float((mk & __float_as_uint(x)) | (~mk & 0xff800000u));
-#else
-    return ((nib >> j) & 1u) ? x : -INFINITY;
-#endif
 }
 // Maxima on raw v_max3_f32 / v_max_f32: fmaxf of a value the compiler cannot
 // prove canonical (a loaded logit, a bitfield select) costs a quieting
 // v_max_f32 x, x per operand in IEEE mode; logits are never signalling NaNs.
-#ifndef OTH_MS_MAX3
-#define OTH_MS_MAX3 1
-#endif
 __device__ __forceinline__ float vmax3(float a, float b, float c) {
-#if OTH_MS_MAX3
     float r;
     asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
-#else
-    return fmaxf(fmaxf(a, b), c);
-#endif
 }
 __device__ __forceinline__ float vmax2(float a, float b) {
-#if OTH_MS_MAX3
     float r;
     asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
-#else
-    return fmaxf(a, b);
-#endif
 }
 // max of v[0..K) (exact in any order): a tree of three-input maxima
 template <int K>

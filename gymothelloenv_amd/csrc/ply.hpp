@@ -28,10 +28,6 @@ namespace oth_dev {
 
 constexpr int PLY_ACTIONS = 0, PLY_RANDOM = 1;
 
-#ifndef OTH_CAP_BITOP3
-#define OTH_CAP_BITOP3 1  // capped_run's cap test as one v_bitop3_b32 per dword (the backend rewrites ~(y - 1) as -y: six ops)
-#endif
-
 // Where the flips' rays come from (a template parameter of the single-ply kernels):
 //   RAYS_MATH  computed per move, no table, no LDS, no barrier (+32 VALU: faster
 //              where one wave per SIMD runs a latency-bound chain, 65,536
@@ -67,6 +63,13 @@ struct RayMath {
     static constexpr uint64_t COL = sum_steps(N, 1, N - 1);       // S from square 0
     static constexpr uint64_t DIAG = sum_steps(N + 1, 1, N - 1);  // SE from square 0
     static constexpr uint64_t ANTI = sum_steps(N - 1, 1, N - 1);  // SW from square N-1, moved to square 0
+    // square s of the board turned by 180 degrees, for any s < 64: an invalid
+    // action's square may lie past N*N - 1 on boards of N < 8, so the result is
+    // kept below 64 (every shift count of up() stays defined; the caller masks
+    // the flips of an invalid action)
+    __device__ __forceinline__ static uint32_t turned(uint32_t s) {
+        return N == 8 ? N * N - 1 - s : (N * N - 1 - s) & 63u;
+    }
     __device__ __forceinline__ static void up(uint32_t s, uint32_t c, uint64_t* ray) {
         const uint32_t row = (1u << N) - 1u;
         const uint64_t gt = ROW1 * (uint64_t)((row << (c + 1)) & row);  // columns > c of every row
@@ -87,11 +90,9 @@ __device__ __forceinline__ uint64_t capped_run(uint64_t ray, uint64_t P, uint64_
     const uint64_t y = ray & ~O;
     const uint64_t ym = y - 1ull;
     const uint64_t run = and3_64(ray, O, ym);
-#if OTH_CAP_BITOP3
-    const uint64_t cap = andn_and_64(y, ym, P);  // y0 if it is an own disc (y & ~(y - 1) & P)
-#else
-    const uint64_t cap = y & ~ym & P;  // y0 if it is an own disc
-#endif
+    // y0 if it is an own disc (y & ~(y - 1) & P): one v_bitop3_b32 per dword (the
+    // backend rewrites a plain ~(y - 1) as -y: six ops)
+    const uint64_t cap = andn_and_64(y, ym, P);
     return cap ? run : 0ull;
 }
 
@@ -109,7 +110,7 @@ __device__ __forceinline__ uint64_t flips_rays(uint64_t P, uint64_t O, const uin
         const uint64_t Pt = OneWord<N>::turn180(P), Ot = OneWord<N>::turn180(O);
         const uint64_t Pl = dn ? Pt : P, Ol = dn ? Ot : O;
         uint64_t ray[4];
-        RayMath<N>::up(dn ? N * N - 1 - s0 : s0, dn ? N - 1 - c0 : c0, ray);
+        RayMath<N>::up(dn ? RayMath<N>::turned(s0) : s0, dn ? N - 1 - c0 : c0, ray);
         uint64_t f = 0;
 #pragma unroll
         for (int d = 0; d < 4; ++d) f |= capped_run(ray[d], Pl, Ol);
@@ -124,7 +125,7 @@ __device__ __forceinline__ uint64_t flips_rays(uint64_t P, uint64_t O, const uin
     if constexpr (RAYS == RAYS_MATH) {  // the turned rays are the up rays of square NN-1-a, column N-1-c
         const uint32_t s = (uint32_t)a & 63u, c = s % N;
         RayMath<N>::up(s, c, ray);
-        RayMath<N>::up(N * N - 1 - s, N - 1 - c, ray + 4);
+        RayMath<N>::up(RayMath<N>::turned(s), N - 1 - c, ray + 4);
     } else {
         static_assert(RAYS == RAYS_HALF || RAYS == RAYS_PAIR, "ray source");  // (PAIR returned above)
         const uint64_t* rt = r - (a & 63) + ((N * N - 1 - (a & 63)) & 63);  // (in the table for any a)

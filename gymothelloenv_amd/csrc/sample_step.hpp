@@ -113,7 +113,7 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step2(uint64_t* __restrict__ b
                                                         int32_t* __restrict__ rewards, uint8_t* __restrict__ dones,
                                                         unsigned long long* __restrict__ wdl, Rng rng, uint64_t ply) {
     constexpr int W = Geo<N>::W;
-    static_assert(W <= 2 && OTH_MS_G == 4, "lane pairs restate k_masked's four lanes of boards of <= 2 words");
+    static_assert(W <= 2 && oth_ms::MS_G == 4, "lane pairs restate k_masked's four lanes of boards of <= 2 words");
     constexpr int NN = N * N;
     ply += rng.ply_off[0];      // graph-region offsets (oth_graph_end); 0 eagerly
     counter += rng.ply_off[1];  // the sample counter's, as k_masked
@@ -169,7 +169,7 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step2(uint64_t* __restrict__ b
             if (dones) dones[e] = (uint8_t)d;
         }
     };
-    if constexpr (VEC && N == 8 && OTH_SS2_STAGE) {  // the wave's 32 rows through LDS: coalesced loads
+    if constexpr (VEC && N == 8) {  // the wave's 32 rows through LDS: coalesced loads
         __shared__ oth_ms::f32x4 stage[(BLOCK / 64) * 32 * oth_ms::PAIR_ROW];
         const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
         oth_ms::f32x4 v[8];
@@ -198,7 +198,7 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step4(uint64_t* __restrict__ b
                                                         float* __restrict__ log_probs, float* __restrict__ entropy,
                                                         int32_t* __restrict__ rewards, uint8_t* __restrict__ dones,
                                                         unsigned long long* __restrict__ wdl, Rng rng, uint64_t ply) {
-    static_assert(Geo<N>::W == 1 && OTH_MS_G == 4, "lane quads are k_masked's four lanes of one-word boards");
+    static_assert(Geo<N>::W == 1 && oth_ms::MS_G == 4, "lane quads are k_masked's four lanes of one-word boards");
     constexpr int NN = N * N;
     ply += rng.ply_off[0];      // graph-region offsets (oth_graph_end); 0 eagerly
     counter += rng.ply_off[1];  // the sample counter's, as k_masked

@@ -70,20 +70,39 @@ class GreedyPolicy(object):
 
 
 class MaxiMinPolicy(object):
-    """simple_policies.py:98-163, searched on the device (max_search_depth 1 ..
-    OTH_MAXIMIN_MAX_DEPTH = 10; the reference's search is exponential in the depth)."""
+    """simple_policies.py:98-163, searched on the device.
+
+    max_search_depth <= 0: the reference's search stops at the root (depth 0 >=
+    max_search_depth, :117-126) and get_action returns None -- no device call.
+    1 .. OTH_MAXIMIN_MAX_DEPTH (10): the device search.  Deeper searches raise
+    (the device's explicit stack holds 10 levels).  The search is one lane per
+    board and exponential in the depth: about b**depth leaf evaluations for b
+    moves per position (8x8 middle games: b ~ 10, so depth 7 is ~10**7 leaves
+    for ONE board, seconds of one GPU lane); DEEP_WARN_LEAVES bounds what runs
+    without a warning."""
+
+    DEEP_WARN_LEAVES = 10 ** 6
 
     def __init__(self, max_search_depth=1):
         from ._lib import OTH_MAXIMIN_MAX_DEPTH
-        if not 1 <= int(max_search_depth) <= OTH_MAXIMIN_MAX_DEPTH:
-            raise ValueError("max_search_depth must be in 1 .. %d on the device" % OTH_MAXIMIN_MAX_DEPTH)
+        if int(max_search_depth) > OTH_MAXIMIN_MAX_DEPTH:
+            raise ValueError("max_search_depth must be at most %d on the device" % OTH_MAXIMIN_MAX_DEPTH)
         self.env = None
         self.max_search_depth = int(max_search_depth)
 
     def reset(self, env):
         self.env = _base(env)
+        n = getattr(self.env, "board_size", 8)
+        b = max(2, n * n // 6)  # a typical middle-game move count (8x8: ~10)
+        if self.max_search_depth > 0 and b ** self.max_search_depth > self.DEEP_WARN_LEAVES:
+            import warnings
+            warnings.warn("MaxiMinPolicy(%d) on %dx%d boards searches ~%.0e leaves per move on one GPU lane; "
+                          "middle-game moves can take seconds to minutes" %
+                          (self.max_search_depth, n, n, float(b ** self.max_search_depth)), RuntimeWarning)
 
     def get_action(self, obs):
+        if self.max_search_depth <= 0:
+            return None  # search(depth=0) returns (count, None) at once (:117-126)
         vec = self.env._vec
         self.env._sync()
         a = int(vec.policy_actions("maximin%d" % self.max_search_depth).cpu()[0])

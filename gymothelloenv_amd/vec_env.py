@@ -152,7 +152,7 @@ class VecOthelloEnv(object):
     def step_policy(self, policy="random", n_plies=1, actions=None, rewards=None, dones=None, record=True):
         """n_plies plies where every board's mover plays `policy` on the device
         (RandomPolicy simple_policies.py:37-41, GreedyPolicy :69-92, MaxiMinPolicy
-        :98-163 as 'maximin1'..'maximin3').
+        :98-163 as 'maximin1'..'maximin10').
 
         Returns (actions, rewards, dones) of shape (n_plies, E) (None if not recorded)."""
         pol = _POLICIES[policy] if isinstance(policy, str) else int(policy)
@@ -215,7 +215,7 @@ class VecOthelloEnv(object):
         return self.policy_actions("greedy")
 
     def policy_actions(self, policy="greedy"):
-        """The move of a scripted policy ('greedy', 'maximin1'..'maximin3';
+        """The move of a scripted policy ('greedy', 'maximin1'..'maximin10';
         simple_policies.py:57-163) for the side to move on every board."""
         out = self._i32(self.num_envs)
         L.check(self._lib.oth_policy_actions(self._h, _POLICIES[policy], _ptr(out), self._stream()),

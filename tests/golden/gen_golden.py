@@ -452,6 +452,44 @@ def gen_maximin_deep(othello, simple_policies):
     np.savez_compressed(os.path.join(OUT, "maximin_deep.npz"), **out)
 
 
+def gen_maximin_deeper(othello, simple_policies):
+    """MaxiMinPolicy(depth) at depth 0 and 6..10 (simple_policies.py:98-163):
+    depth 0 returns no move (:117-126); depths 6..10 on 4x4 boards from any
+    position, 5x5 at depth 6..7 and 6x6 / 8x8 at depth 6 on positions with at
+    most `max_empty` empty squares (the reference's search is exponential in
+    the depth; late positions keep it to minutes)."""
+    out = {}
+    plan = [(4, d, 12, 16) for d in (6, 7, 8, 9, 10)] + [(5, 6, 10, 16), (5, 7, 9, 10), (6, 6, 11, 16),
+                                                          (8, 6, 9, 6), (6, 0, 40, 8)]
+    for n, depth, max_empty, positions in plan:
+        rnd = np.random.RandomState(131 * n + depth)
+        env = othello.OthelloBaseEnv(board_size=n, mute=True)
+        pol = simple_policies.MaxiMinPolicy(depth)
+        pol.reset(env)
+        blacks, whites, turns, acts = [], [], [], []
+        while len(acts) < positions:
+            env.reset()
+            done = False
+            while not done and len(acts) < positions:
+                b, w, t, _ = snapshot(env, n)
+                empty = n * n - int(np.count_nonzero(env.board_state))
+                if empty <= max_empty and rnd.rand() < 0.5:
+                    a = pol.get_action(env.get_observation())
+                    blacks.append(b)
+                    whites.append(w)
+                    turns.append(t)
+                    acts.append(-1 if a is None else int(a))
+                pm = env.possible_moves
+                _, _, done, _ = env.step(int(pm[rnd.randint(0, len(pm))]))
+        key = "N%d_d%d_" % (n, depth)
+        out[key + "black"] = np.array(blacks, dtype=np.uint64)
+        out[key + "white"] = np.array(whites, dtype=np.uint64)
+        out[key + "turn"] = np.array(turns, dtype=np.int8)
+        out[key + "action"] = np.array(acts, dtype=np.int32)
+        print("maximin N=%d depth=%d: %d positions" % (n, depth, len(acts)), flush=True)
+    np.savez_compressed(os.path.join(OUT, "maximin_deeper.npz"), **out)
+
+
 def install_learner_shims():
     """Stand-ins for what the learners' modules import but the policy heads never
     use: torch.utils.tensorboard (ppo.py:7; tensorboard is absent), the
@@ -589,6 +627,9 @@ def main():
     if sys.argv[1:] == ["maximin_deep"]:
         gen_maximin_deep(othello, simple_policies)
         return
+    if sys.argv[1:] == ["maximin_deeper"]:
+        gen_maximin_deeper(othello, simple_policies)
+        return
     gen_kat(othello)
     gen_trajectories(othello)
     gen_greedy(othello, simple_policies, util)
@@ -597,6 +638,7 @@ def main():
     gen_vs(othello)
     gen_maximin(othello, simple_policies)
     gen_maximin_deep(othello, simple_policies)
+    gen_maximin_deeper(othello, simple_policies)
     gen_masked(othello)
 
 

@@ -148,7 +148,6 @@ int host_greedy_planes(int n, int E, const uint64_t* mover, const uint64_t* opp,
     return 0;
 }
 int host_select(uint64_t x, int k) { return select64(x, k); }
-#if OTH_SELECT == 2
 // select64_tab with the sel8 table as k_play_rand stages it in LDS
 int host_select_tab(uint64_t x, int k) {
     static uint64_t tab[256];
@@ -159,7 +158,6 @@ int host_select_tab(uint64_t x, int k) {
     }
     return select64_tab(x, k, reinterpret_cast<const uint8_t*>(tab));
 }
-#endif
 void host_philox4(uint64_t seed, uint32_t id, uint64_t ctr, uint32_t purpose, uint32_t* out) {
     U4 u = philox4(seed, id, ctr, purpose);
     out[0] = u.x;

@@ -87,16 +87,14 @@ def test_flips_host_build(hostlib, n):
     np.testing.assert_array_equal(out, opp & ~s.boards[:, :W])
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3])
-def test_select_variants_every_rank(variant):
-    """Every select form (OTH_SELECT=1 binary search, 2 byte-parallel, 3 = 2 with
-    the bit inside the byte from k_play_rand's sel8 table), every rank k of dense
-    and sparse (legal-mask-like) words."""
-    L = build_host(os.path.join(HERE, "host", "libbitboard_host_sel%d.so" % min(variant, 2)),
-                   ["-DOTH_SELECT=%d" % min(variant, 2)])
-    sel = L.host_select_tab if variant == 3 else L.host_select
+@pytest.mark.parametrize("variant", ["select64", "select64_tab"])
+def test_select_variants_every_rank(hostlib, variant):
+    """Both select forms (byte-parallel select64, and select64_tab with the bit
+    inside the byte from k_play_rand's sel8 table), every rank k of dense and
+    sparse (legal-mask-like) words."""
+    sel = hostlib.host_select_tab if variant == "select64_tab" else hostlib.host_select
     sel.argtypes = [ctypes.c_uint64, ctypes.c_int]
-    rng = np.random.RandomState(variant)
+    rng = np.random.RandomState(len(variant))
     words = [1, 1 << 63, (1 << 64) - 1, 0x8000000000000001, 0x0101010101010101, 0xF0]
     for _ in range(1500):
         dens = rng.choice([0.05, 0.15, 0.5, 0.9])

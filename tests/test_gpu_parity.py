@@ -454,12 +454,15 @@ def test_vs_rollout_replays_on_oracle(torch_cuda, n, opp, init_rand):
     np.testing.assert_array_equal(env.counts().cpu().numpy(), wdl)
 
 
-@pytest.mark.parametrize("n,depth", [(6, 1), (6, 2), (6, 3), (8, 1), (8, 2), (8, 3), (6, 4), (6, 5), (8, 4)])
+@pytest.mark.parametrize("n,depth", [(6, 1), (6, 2), (6, 3), (8, 1), (8, 2), (8, 3), (6, 4), (6, 5), (8, 4),
+                                     (4, 6), (4, 7), (4, 8), (4, 9), (4, 10), (5, 6), (5, 7), (6, 6), (8, 6)])
 def test_maximin_actions_match_reference(torch_cuda, golden_dir, n, depth):
     """MaxiMinPolicy(depth).get_action (simple_policies.py:98-163) on device;
-    depth >= 4 runs the explicit-stack search (maximin_search)."""
+    depth >= 4 runs the explicit-stack search (maximin_search); depths 6..10
+    on the late positions of maximin_deeper.npz."""
     torch = torch_cuda
-    g = np.load(os.path.join(golden_dir, "maximin.npz" if depth <= 3 else "maximin_deep.npz"))
+    g = np.load(os.path.join(golden_dir, "maximin.npz" if depth <= 3 else
+                             ("maximin_deep.npz" if depth <= 5 else "maximin_deeper.npz")))
     k = "N%d_d%d_" % (n, depth)
     b, w, t, a = g[k + "black"], g[k + "white"], g[k + "turn"], g[k + "action"]
     env = make_env(torch, len(a), n)
@@ -607,8 +610,8 @@ def test_single_ply_kernels_both_ray_sources(torch_cuda, n, E):
     """The single-ply kernels (ply.hpp) compute their rays up to 65,536 boards
     and read the handle's LDS-staged table beyond: both equal the oracle for
     external actions (legal, illegal, out of range; both sudden-death modes)
-    and for one-ply random play, ragged E included; dones views at every byte
-    offset (the kernels pack a lane quad's dones into one dword when aligned)."""
+    and for one-ply random play, ragged E included; a dones view at every byte
+    offset, guarded on both sides against writes outside the view."""
     torch = torch_cuda
     rng = np.random.RandomState(E + n)
     for sd in (True, False):
@@ -620,7 +623,7 @@ def test_single_ply_kernels_both_ray_sources(torch_cuda, n, E):
             wild = (rng.rand(E) < 0.1) | ~lb.any(axis=1)
             acts = np.where(wild, rng.randint(-2, n * n + 2, size=E), pick).astype(np.int32)
             orw, od, _ = oracle.step(s, flags_of(sd, False, True), acts, seed=9, ply=p)
-            off = p % 4  # dones at every byte offset (packed dword stores only where 4-aligned)
+            off = p % 4  # a dones view at every byte offset
             dbuf = torch.full((E + 4,), 7, dtype=torch.uint8, device="cuda")
             _, rew, dn, _ = env.step(torch.from_numpy(acts).cuda(), dones=dbuf[off:off + E], observe=False)
             np.testing.assert_array_equal(rew.cpu().numpy(), orw)
