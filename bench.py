@@ -155,12 +155,16 @@ def cpu_baseline(seconds, board_size=8, threads=None):
 
 def load_pmc(workload):
     """The rocprofv3 PMC summary of this workload committed under profiles/
-    (tools/pmc_profile.sh + tools/pmc_summarize.py), or None."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    try:
-        return json.load(open(p)).get(workload)
-    except Exception:
-        return None
+    (tools/pmc_profile.sh / tools/gpu_prof_configs.sh + tools/pmc_summarize.py),
+    or None."""
+    for f in ("pmc_traffic.json", "pmc_configs.json"):
+        try:
+            rec = json.load(open(os.path.join(ROOT, "profiles", f))).get(workload)
+        except Exception:
+            rec = None
+        if rec:
+            return rec
+    return None
 
 
 def play_kernel_name(n, policy, record):
@@ -427,6 +431,9 @@ def make_record(args, world, G, E, P, n, record, wall_max, kern_ms, wdl_total, s
         "roofline": {"bound": "hbm", "limiter": "integer VALU issue (see valu)",
                      "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS if achieved else None,
+                     "achieved_kind": "equivalent bandwidth: SURVEY §8(d)'s algorithmic bytes over the launch time; "
+                                      "the fused launch keeps boards in registers, so HBM moves `traffic` only",
+                     "moved_GBps": pmc["hbm_bytes_per_launch"] / avg_launch_s / 1e9 if pmc and avg_launch_s else None,
                      "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
                      "traffic_source": pmc.get("source") if pmc else None,
                      "kernel": play_kernel_name(n, args.policy, record),
@@ -551,6 +558,88 @@ def single_ply(env, policy, E, W, dev, stream, k=64):
             "algorithmic_GBps": gbs, "frac": gbs / HBM_PEAK_GBPS}
 
 
+def play_line(policy, n, E, P, init_rand, dev, stream, launches=20, warm=3):
+    """One oth_step_policy launch of P plies over E boards with auto-reset and
+    every per-ply output stored (k_play_rand<N, policy> for N <= 8,
+    k_play_rand_w<N> above): BASELINE config 3 (greedy, 8x8, 0..init_rand-ply
+    random openings as bench's greedy) and config 5 (random, 6x6 / 10x10).
+    HIP events around `launches` back-to-back launches on the launch stream."""
+    import torch
+
+    from gymothelloenv_amd import VecOthelloEnv
+    from gymothelloenv_amd.vec_env import nwords
+    W = nwords(n)
+    env = VecOthelloEnv(E, board_size=n, auto_reset=True, seed=0, initial_rand_steps=init_rand, device=dev)
+    env.reset()
+    acts = torch.empty(P, E, dtype=torch.int32, device=dev)
+    rews = torch.empty(P, E, dtype=torch.int32, device=dev)
+    dns = torch.empty(P, E, dtype=torch.uint8, device=dev)
+
+    def one(i):
+        env.step_policy(policy, n_plies=P, actions=acts, rewards=rews, dones=dns)
+    for i in range(warm):
+        one(i)
+    us = _time_launches(stream, one, launches)
+    wdl = [int(x) for x in env.counts().cpu().tolist()]
+    env.close()
+    bps = step_bytes(W)
+    gbs = E * P * bps / (us * 1e-6) / 1e9
+    workload = "%s-play-%dx%d-E%d-P%d" % (policy, n, n, E, P)
+    return {"workload": workload, "kernel": play_kernel_name(n, policy, True), "boards": E, "board_size": n,
+            "plies_per_launch": P, "initial_rand_steps": init_rand, "avg_launch_us": us, "us_per_ply": us / P,
+            "value": E * P / (us * 1e-6), "unit": "env-steps/s", "launches_timed": launches, "wdl": wdl,
+            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": gbs / HBM_PEAK_GBPS, "algorithmic_bytes_per_env_step": bps,
+                         "fused_bytes_per_launch": fused_bytes_per_launch(E, W, P),
+                         "pmc": load_pmc(workload)}}
+
+
+def observe_bytes(n, E, layout, esize):
+    """get_observation / make_state: the (E, planes, N, N) output written once,
+    the board words (16W), meta (2) and, for the layouts with a legal plane,
+    possible_moves (8W) read once per board."""
+    W = (n * n + 63) // 64
+    planes = {"board": 1, "board_legal": 2, "make_state": 4, "absolute": 1}[layout]
+    reads = 16 * W + 2 + (8 * W if layout in ("board_legal", "make_state") else 0)
+    return E * (planes * n * n * esize + reads)
+
+
+def observe_lines(n, sizes, dev, stream, launches=50):
+    """oth_observe (k_observe_w) into a preallocated tensor: int64 BOARD (the
+    Gym-style get_observation, othello.py:363-378) and f32 MAKE_STATE
+    (util.make_state, util.py:48-74), mid-game boards; HIP graph of `launches`
+    launches (the short launches back to back), median of 5 replays."""
+    import torch
+
+    from gymothelloenv_amd import VecOthelloEnv
+    out = []
+    for E in sizes:
+        env = VecOthelloEnv(E, board_size=n, auto_reset=True, seed=3, device=dev)
+        env.step_policy("random", n_plies=25, record=False)
+        for layout, dt, esize in (("board", torch.int64, 8), ("make_state", torch.float32, 4)):
+            shape = (E, n, n) if layout == "board" else (E, 4, n, n)
+            buf = torch.empty(shape, dtype=dt, device=dev)
+            for _ in range(3):
+                env.observe(layout, dt, out=buf)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(launches):
+                    env.observe(layout, dt, out=buf)
+            us = statistics.median([_time_launches(stream, lambda i: g.replay(), 1) / launches for _ in range(5)])
+            del g
+            b = observe_bytes(n, E, layout, esize)
+            workload = "observe-%s-%s-%dx%d-E%d" % (layout, str(dt).replace("torch.", ""), n, n, E)
+            out.append({"workload": workload, "kernel": "k_observe_w<%d,%s,%s>" % (n, layout, str(dt)),
+                        "boards": E, "avg_launch_us": us, "algorithmic_bytes_per_launch": b,
+                        "timing": "HIP graph of %d launches, median of 5 replays" % launches,
+                        "roofline": {"bound": "hbm", "achieved": b / (us * 1e-6) / 1e9, "peak": HBM_PEAK_GBPS,
+                                     "unit": "GB/s", "frac": b / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS,
+                                     "pmc": load_pmc(workload)}})
+            del buf
+        env.close()
+    return out
+
+
 def side_measurements(env, policy, E, n, W, dev, stream):
     """Beside the headline (never `value`): the per-step paths with the state
     through HBM every ply -- oth_step with external actions (`step_external`)
@@ -563,6 +652,12 @@ def side_measurements(env, policy, E, n, W, dev, stream):
 
     from gymothelloenv_amd import VecOthelloEnv
     out = {"step_external": [step_external(Eb, n, dev, stream) for Eb in (E, 1048576)]}
+    # BASELINE configs 3 (greedy, 8x8) and 5 (random, 6x6 and 10x10) at their stated 65,536 boards
+    out["configs"] = {"config3_greedy": [play_line("greedy", 8, CONFIG2_BOARDS, P, 10, dev, stream)
+                                         for P in (10, 100)],
+                      "config5_random": [play_line("random", nb, CONFIG2_BOARDS, 100, 0, dev, stream)
+                                         for nb in (6, 10)]}
+    out["observe"] = observe_lines(n, (E, 1048576), dev, stream)
     big = VecOthelloEnv(1048576, board_size=n, auto_reset=True, seed=0, device=dev)
     big.step_policy(policy, n_plies=20, record=False)
     out["single_ply_launches"] = [single_ply(env, policy, E, W, dev, stream),

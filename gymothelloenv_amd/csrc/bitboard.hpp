@@ -917,8 +917,11 @@ struct OneWord {
     // GreedyPolicy.get_action (simple_policies.py:69-92): the candidate (a
     // square of `legal`) flipping the most discs, the lowest of equal counts
     // (np.argmax); -1 without candidates.  The eight run lengths are summed on
-    // bit planes (at most 19 flips on a board of N <= 8: 5 planes), then the
+    // bit planes (at most 18 flips on a board of N <= 8: 5 planes), then the
     // largest total among the candidates is found plane by plane from the top.
+    // Opposite directions are added first: both runs lie on one line through
+    // the square, between two own discs, so their sum is at most N - 2 <= 6 and
+    // stays 3 bits (no carry out of the first adders).
     // The planes are plain 64-bit words: on dword pairs (U2) the gfx950 backend
     // miscompiled them inside k_play ("A compiler hazard";
     // tests/test_gpu_hazards.py pins the position).
@@ -932,12 +935,26 @@ struct OneWord {
         run_len<-N>(t[5], n[5]);
         run_len<-N - 1>(t[6], n[6]);
         run_len<-N + 1>(t[7], n[7]);
-        uint64_t s4[4][4], s5[2][5], tot[5];
+#ifndef OTH_GREEDY_AXIS_SUM
+#define OTH_GREEDY_AXIS_SUM 1  // A/B of round 4 (0: round 3's pairing, 4-bit first sums)
+#endif
+        uint64_t tot[5];
+        if constexpr (OTH_GREEDY_AXIS_SUM) {
+            static_assert(N - 2 <= 7, "an axis' two runs fit 3 bits");
+            uint64_t s3[4][3], s4[2][4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) add_planes<3, 3, 4>(n[2 * i], n[2 * i + 1], s4[i]);
-        add_planes<4, 4, 5>(s4[0], s4[1], s5[0]);
-        add_planes<4, 4, 5>(s4[2], s4[3], s5[1]);
-        add_planes<5, 5, 5>(s5[0], s5[1], tot);
+            for (int i = 0; i < 4; ++i) add_planes<3, 3, 3>(n[i], n[i + 4], s3[i]);  // d and its opposite d + 4
+            add_planes<3, 3, 4>(s3[0], s3[1], s4[0]);
+            add_planes<3, 3, 4>(s3[2], s3[3], s4[1]);
+            add_planes<4, 4, 5>(s4[0], s4[1], tot);
+        } else {
+            uint64_t s4[4][4], s5[2][5];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) add_planes<3, 3, 4>(n[2 * i], n[2 * i + 1], s4[i]);
+            add_planes<4, 4, 5>(s4[0], s4[1], s5[0]);
+            add_planes<4, 4, 5>(s4[2], s4[3], s5[1]);
+            add_planes<5, 5, 5>(s5[0], s5[1], tot);
+        }
         uint64_t cand = legal;
 #pragma unroll
         for (int i = 4; i >= 0; --i) {

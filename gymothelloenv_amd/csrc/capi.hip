@@ -163,7 +163,7 @@ int oth_create(int32_t n_envs, int32_t board_size, uint32_t flags, uint64_t seed
     const size_t ctr_bytes = (size_t)OTH_GRAPH_SLOTS * 2 * sizeof(uint64_t);
     if (err == hipSuccess) err = hipMalloc((void**)&env->ctr_slots, ctr_bytes);
     if (err == hipSuccess) err = hipMemset(env->ctr_slots, 0, ctr_bytes);
-    if (err == hipSuccess && env->W == 1) err = hipMalloc((void**)&env->rays, 8 * 64 * sizeof(uint64_t));
+    if (err == hipSuccess && env->W == 1) err = hipMalloc((void**)&env->rays, TABLE_WORDS * sizeof(uint64_t));
     env->cur_off = env->ctr_slots;
     env->graph_slot = 0;
     env->slots_used = 1;
@@ -388,7 +388,7 @@ int oth_graph_offsets(const oth_env* env, int32_t slot, uint64_t* out) {
 int oth_observe(oth_env* env, int32_t layout, int32_t dtype, void* out, oth_stream_t stream) {
     OTH_CHECK_ENV(env);
     if (!out) return fail(OTH_EINVAL, "out is NULL");
-    if (layout < OTH_OBS_BOARD || layout > OTH_OBS_ABSOLUTE) return fail(OTH_EINVAL, "unknown layout");
+    if (layout < OTH_OBS_BOARD || layout > OTH_OBS_LEGAL) return fail(OTH_EINVAL, "unknown layout");
     if (dtype < OTH_I8 || dtype > OTH_F64) return fail(OTH_EINVAL, "unknown dtype");
     return with_n(env->n, [&](auto NC) {
         return launch_observe<decltype(NC)::value>(env, layout, dtype, out, (hipStream_t)stream);

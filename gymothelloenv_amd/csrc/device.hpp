@@ -999,7 +999,8 @@ __device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_
     if constexpr (POLICY == OTH_POLICY_RANDOM) {
         a = pick(u);  // RandomPolicy (simple_policies.py:37-41); L != 0
     } else if constexpr (OPEN) {
-        if (meta & 0xff00u) a = pick(action_draw(rng.seed, id, g));
+        // a random-opening ply draws u = action_draw(seed, id, g), from the caller's block
+        if (meta & 0xff00u) a = pick(u);
         else a = OneWord<N>::greedy(eng.t, L);
     } else {
         a = OneWord<N>::greedy(eng.t, L);
@@ -1062,26 +1063,43 @@ __device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_
     }
 }
 
+#ifndef OTH_PLAY_TABLES
+#define OTH_PLAY_TABLES 1  // A/B of round 4: k_play_rand's LDS tables copied from the handle's (0: built per block)
+#endif
+// tables: the handle's ray + sel8 tables (oth_env::rays, k_fill_rays), copied into
+// LDS by one 16-byte and one 8-byte load per thread, issued with the board's loads
 template <int N, int POLICY = OTH_POLICY_RANDOM>
 __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
                                                      uint64_t* __restrict__ legal, int E, uint32_t flags, int plies,
                                                      int32_t* __restrict__ actions, int32_t* __restrict__ rewards,
                                                      uint8_t* __restrict__ dones,
-                                                     unsigned long long* __restrict__ wdl, Rng rng, uint64_t ply0) {
+                                                     unsigned long long* __restrict__ wdl, Rng rng, uint64_t ply0,
+                                                     const uint64_t* __restrict__ tables) {
     static_assert(Geo<N>::W == 1, "one-word boards");
+    static_assert(BLOCK == 256 && Fills<N>::RAY_WORDS == 2 * BLOCK, "two ray words and one sel8 word a thread");
     ply0 += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
     __shared__ __attribute__((aligned(16))) uint64_t lds_rays[Fills<N>::RAY_WORDS];
     __shared__ __attribute__((aligned(16))) uint64_t lds_sel[256];
-    for (int i = threadIdx.x; i < 256; i += BLOCK) lds_sel[i] = sel8_word((uint32_t)i);
     const uint8_t* sel8 = reinterpret_cast<const uint8_t*>(lds_sel);
-    fill_rays<N, turned_rays<Fills<N>>::value>(lds_rays);  // (its barrier covers lds_sel)
     const int e = blockIdx.x * BLOCK + threadIdx.x;
+    Lane<N> s;
+#if OTH_PLAY_TABLES
+    const ulonglong2 tr = reinterpret_cast<const ulonglong2*>(tables)[threadIdx.x];
+    const uint64_t ts = tables[Fills<N>::RAY_WORDS + threadIdx.x];
+    if (e < E) load_lane<N>(s, boards, meta, legal, e);
+    reinterpret_cast<ulonglong2*>(lds_rays)[threadIdx.x] = tr;
+    lds_sel[threadIdx.x] = ts;
+    __syncthreads();
+#else
+    for (int i = threadIdx.x; i < 256; i += BLOCK) lds_sel[i] = sel8_word((uint32_t)i);
+    fill_rays<N, turned_rays<Fills<N>>::value>(lds_rays);  // (its barrier covers lds_sel)
+    (void)tables;
+    if (e < E) load_lane<N>(s, boards, meta, legal, e);
+#endif
     uint32_t cb = 0, cd = 0, cw = 0;
     if (e < E) {
         const uint32_t id = rng.id_base + (uint32_t)e;
         const Fills<N> eng(0, lds_rays);
-        Lane<N> s;
-        load_lane<N>(s, boards, meta, legal, e);
         const bool tw0 = (s.meta & M_TURN_WHITE) != 0;
         uint64_t M = tw0 ? s.white.w[0] : s.black.w[0];
         uint64_t O = tw0 ? s.black.w[0] : s.white.w[0];
@@ -1115,8 +1133,30 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
             done_p += E;
         };
         const NoFill nofill;
-        if (POLICY != OTH_POLICY_RANDOM) {  // scripted policy: draws only on opening plies
-            for (int p = 0; p < plies; ++p) ply(p, 0u, nofill);
+        if constexpr (POLICY != OTH_POLICY_RANDOM) {  // scripted policy: draws only on opening plies
+#ifndef OTH_OPEN_BLOCK
+#define OTH_OPEN_BLOCK 1  // A/B of round 4 (0: round 3's Philox evaluation per opening ply)
+#endif
+            if constexpr (OPEN && !OTH_OPEN_BLOCK) {
+                for (int p = 0; p < plies; ++p) ply(p, action_draw(rng.seed, id, ply0 + (uint64_t)p), nofill);
+            } else if constexpr (OPEN) {
+                // an opening ply's draw is word g % 4 of Philox block g / 4 (action_draw's
+                // value); the block is computed once per group of four plies, at the first
+                // ply where some board of the wave has opening plies left (uniform branch):
+                // one Philox evaluation per 4 plies instead of one per ply
+                U4 blk{0u, 0u, 0u, 0u};
+                uint64_t held = ~0ull;  // the block in blk (wave-uniform)
+                for (int p = 0; p < plies; ++p) {
+                    const uint64_t g = ply0 + (uint64_t)p;
+                    if ((g >> 2) != held && __any((mt & 0xff00u) != 0)) {
+                        blk = philox4(rng.seed, id, g >> 2, RNG_ACTION);
+                        held = g >> 2;
+                    }
+                    ply(p, pick4(blk, (uint32_t)(g & 3)), nofill);
+                }
+            } else {
+                for (int p = 0; p < plies; ++p) ply(p, 0u, nofill);
+            }
             return;
         }
         int p = 0;
@@ -1587,6 +1627,8 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const uint64_t* __restrict__ 
         int v;
         if (layout == OTH_OBS_ABSOLUTE) {
             v = isw - isb;
+        } else if (layout == OTH_OBS_LEGAL) {
+            v = (int)((legal[e * W + wi] >> bi) & 1u);
         } else if (layout == OTH_OBS_MAKE_STATE) {
             if (plane == 0) {
                 v = isb;
@@ -1657,21 +1699,25 @@ __device__ __forceinline__ void put_quad(T* out, uint32_t q, int v0, int v1, int
 // wave (round 2's k_observe_q, each wave waiting on its own board's loads
 // before one 1-KiB store) reached 2.6 TB/s for make_state f32 at 1,048,576
 // boards; one wave's loads feeding 64 boards' stores, 5.0 (a plain fill: 6.9).
-template <int N, int LAYOUT, typename T>
+// BPW boards per wave (64, or 16 for small launches: four times the waves, each
+// streaming a quarter of the region, so the store streams start sooner and
+// more of them are in flight).
+template <int N, int LAYOUT, typename T, int BPW = 64>
 __global__ __launch_bounds__(BLOCK) void k_observe_w(const uint64_t* __restrict__ boards,
                                                      const uint16_t* __restrict__ meta,
                                                      const uint64_t* __restrict__ legal, int E, T* __restrict__ out) {
+    static_assert(BPW == 4 || BPW == 8 || BPW == 16 || BPW == 32 || BPW == 64, "boards per wave");
     constexpr int W = Geo<N>::W;
     constexpr int NN = N * N;
     static_assert(NN % 4 == 0, "quads of squares");
     constexpr int Q = NN / 4;
     constexpr int PLANES = LAYOUT == OTH_OBS_BOARD_LEGAL ? 2 : (LAYOUT == OTH_OBS_MAKE_STATE ? 4 : 1);
     constexpr int PQ = PLANES * Q;  // quads per board
-    constexpr bool NEED_L = LAYOUT == OTH_OBS_BOARD_LEGAL || LAYOUT == OTH_OBS_MAKE_STATE;
+    constexpr bool NEED_L = LAYOUT == OTH_OBS_BOARD_LEGAL || LAYOUT == OTH_OBS_MAKE_STATE || LAYOUT == OTH_OBS_LEGAL;
     const int lane = threadIdx.x & 63;
-    const long long e0 = (long long)blockIdx.x * BLOCK + threadIdx.x - lane;  // the wave's first board
-    if (e0 >= E) return;                                                     // wave-uniform
-    const long long e = e0 + lane;
+    const long long e0 = ((long long)blockIdx.x * BLOCK + threadIdx.x - lane) / 64 * BPW;  // the wave's first board
+    if (e0 >= E) return;                                                                 // wave-uniform
+    const long long e = lane < BPW ? e0 + lane : E;  // lanes past BPW load nothing
     uint64_t bw[W], ww[W], lw[W];
     uint32_t fl = 0;  // bit 0: white to move; bit 1: more than one legal move (util.py:55)
 #pragma unroll
@@ -1689,7 +1735,7 @@ __global__ __launch_bounds__(BLOCK) void k_observe_w(const uint64_t* __restrict_
         }
         fl = ((meta[e] & M_TURN_WHITE) ? 1u : 0u) | (cnt > 1 ? 2u : 0u);
     }
-    const int nb = (int)(E - e0 < 64 ? E - e0 : 64);
+    const int nb = (int)(E - e0 < BPW ? E - e0 : BPW);
     const int total = nb * PQ;
     T* base = out + (size_t)e0 * PQ * 4;
     auto fetch = [&](const uint64_t (&x)[W], int kb, int wi) __attribute__((always_inline)) {
@@ -1715,7 +1761,10 @@ __global__ __launch_bounds__(BLOCK) void k_observe_w(const uint64_t* __restrict_
         uint32_t nl = 0;
         if constexpr (NEED_L) nl = (uint32_t)(fetch(lw, kb, wi) >> bi) & 0xFu;
         int v[4];
-        if constexpr (LAYOUT == OTH_OBS_ABSOLUTE) {  // othello.py:257
+        if constexpr (LAYOUT == OTH_OBS_LEGAL) {  // possible_moves
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = (int)((nl >> j) & 1u);
+        } else if constexpr (LAYOUT == OTH_OBS_ABSOLUTE) {  // othello.py:257
 #pragma unroll
             for (int j = 0; j < 4; ++j) v[j] = (int)((nwk >> j) & 1u) - (int)((nbk >> j) & 1u);
         } else if constexpr (LAYOUT == OTH_OBS_MAKE_STATE) {  // util.py:48-74

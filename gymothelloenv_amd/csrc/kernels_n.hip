@@ -254,29 +254,45 @@ int launch_legal_moves(int n, const uint64_t* mover, const uint64_t* opp, uint64
     return after_launch("oth_legal_moves");
 }
 
-// one wave per 64 boards (k_observe_w), vector stores of 4 squares: N*N % 4 == 0
-template <int N, typename T>
-void launch_observe_w(oth_env* env, int layout, void* out, hipStream_t st) {
-    T* o = static_cast<T*>(out);
-    const dim3 gw(grid_for(((long long)env->E + 63) / 64 * 64));
+#ifndef OTH_OBS_SMALL_E
+#define OTH_OBS_SMALL_E 262144  // observations of fewer boards: OTH_OBS_BPW boards per wave (k_observe_w)
+#endif
+#ifndef OTH_OBS_BPW
+#define OTH_OBS_BPW 16
+#endif
+
+// one wave per BPW boards (k_observe_w), vector stores of 4 squares: N*N % 4 == 0
+template <int N, typename T, int BPW>
+void launch_observe_bpw(oth_env* env, int layout, T* o, hipStream_t st) {
+    const dim3 gw(grid_for(((long long)env->E + BPW - 1) / BPW * 64));
     switch (layout) {
         case OTH_OBS_BOARD:
-            hipLaunchKernelGGL((k_observe_w<N, OTH_OBS_BOARD, T>), gw, dim3(BLOCK), 0, st, env->boards, env->meta,
-                               env->legal, env->E, o);
+            hipLaunchKernelGGL((k_observe_w<N, OTH_OBS_BOARD, T, BPW>), gw, dim3(BLOCK), 0, st, env->boards,
+                               env->meta, env->legal, env->E, o);
             break;
         case OTH_OBS_BOARD_LEGAL:
-            hipLaunchKernelGGL((k_observe_w<N, OTH_OBS_BOARD_LEGAL, T>), gw, dim3(BLOCK), 0, st, env->boards,
+            hipLaunchKernelGGL((k_observe_w<N, OTH_OBS_BOARD_LEGAL, T, BPW>), gw, dim3(BLOCK), 0, st, env->boards,
                                env->meta, env->legal, env->E, o);
             break;
         case OTH_OBS_MAKE_STATE:
-            hipLaunchKernelGGL((k_observe_w<N, OTH_OBS_MAKE_STATE, T>), gw, dim3(BLOCK), 0, st, env->boards,
+            hipLaunchKernelGGL((k_observe_w<N, OTH_OBS_MAKE_STATE, T, BPW>), gw, dim3(BLOCK), 0, st, env->boards,
+                               env->meta, env->legal, env->E, o);
+            break;
+        case OTH_OBS_ABSOLUTE:
+            hipLaunchKernelGGL((k_observe_w<N, OTH_OBS_ABSOLUTE, T, BPW>), gw, dim3(BLOCK), 0, st, env->boards,
                                env->meta, env->legal, env->E, o);
             break;
         default:
-            hipLaunchKernelGGL((k_observe_w<N, OTH_OBS_ABSOLUTE, T>), gw, dim3(BLOCK), 0, st, env->boards,
+            hipLaunchKernelGGL((k_observe_w<N, OTH_OBS_LEGAL, T, BPW>), gw, dim3(BLOCK), 0, st, env->boards,
                                env->meta, env->legal, env->E, o);
             break;
     }
+}
+template <int N, typename T>
+void launch_observe_w(oth_env* env, int layout, void* out, hipStream_t st) {
+    T* o = static_cast<T*>(out);
+    if (env->E < OTH_OBS_SMALL_E) launch_observe_bpw<N, T, OTH_OBS_BPW>(env, layout, o, st);
+    else launch_observe_bpw<N, T, 64>(env, layout, o, st);
 }
 
 template <int N>

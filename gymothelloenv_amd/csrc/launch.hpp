@@ -7,6 +7,9 @@
 
 #include "othello_mi355x.h"
 
+// one-word boards: oth_env::rays holds the 8 x 64-word ray table, then the sel8 table
+constexpr int RAY_TABLE_WORDS = 8 * 64, SEL8_WORDS = 256, TABLE_WORDS = RAY_TABLE_WORDS + SEL8_WORDS;
+
 struct oth_env {
     int32_t E;
     int32_t n;
@@ -33,7 +36,8 @@ struct oth_env {
     int32_t graph_slot;       // open region (0: none)
     uint64_t slots_used;      // bit k: slot k belongs to a captured graph (bit 0, eager, always set)
     uint64_t ply_saved;       // eager ply counter while a region is open
-    uint64_t* rays;           // one-word boards: the 8 x 64 ray table of the single-ply kernel (ply.hpp)
+    uint64_t* rays;           // one-word boards: the 8 x 64 ray table (fill_rays<N, true>) then the 256-word
+                              // sel8 table (TABLE_WORDS), read by the single-ply kernels and k_play_rand
 };
 
 namespace oth_host {

@@ -145,11 +145,71 @@ __device__ __forceinline__ uint64_t flips_rays(uint64_t P, uint64_t O, const uin
 }
 
 
+// get_possible_actions (othello.py:313-343) split over a lane pair holding the
+// same board: each lane scans two of the four axes -- lane 0 E/W and S/N, lane
+// 1 the two diagonals -- with the same code (per-lane shift amounts and
+// propagator masks in registers: a 64-bit shift by a VGPR amount is one
+// v_lshl*_b64 like a constant one), and the pair ORs its halves through DPP.
+// Kogge-Stone doubling 1 + 1 + 2 + 2 covers the longest run (N - 2 <= 6).
+struct PairAxes {
+    uint32_t s0, s1;  // the lane's two axis steps
+    uint64_t m0, m1;  // their propagator masks (inner columns, or the board for S/N)
+};
+template <int N>
+__device__ __forceinline__ PairAxes pair_axes(int h) {
+    constexpr uint64_t BD = Geo<N>::BOARD.w[0], IN = Geo<N>::INNER.w[0];
+    return h ? PairAxes{N + 1u, N - 1u, IN, IN} : PairAxes{1u, (uint32_t)N, IN, BD};
+}
+__device__ __forceinline__ uint64_t and_or_64(uint64_t a, uint64_t b, uint64_t c) {  // (a & b) | c
+    const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, 0xEA);
+    const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), 0xEA);
+    return ((uint64_t)hi << 32) | lo;
+}
+// squares one step past the fills of the mover P through p1, both directions of step s
+__device__ __forceinline__ uint64_t axis_var(uint64_t P, uint64_t p1, uint32_t s) {
+    const uint64_t p2 = p1 & (p1 << s);
+    uint64_t x = (P << s) & p1;
+    x = and_or_64(p1, x << s, x);
+    x = and_or_64(p2, x << (2 * s), x);
+    x = and_or_64(p2, x << (2 * s), x);
+    const uint64_t up = x << s;
+    const uint64_t p2m = p2 >> s;
+    x = (P >> s) & p1;
+    x = and_or_64(p1, x >> s, x);
+    x = and_or_64(p2m, x >> (2 * s), x);
+    x = and_or_64(p2m, x >> (2 * s), x);
+    return up | (x >> s);
+}
+__device__ __forceinline__ uint64_t pair_or(uint64_t x) {  // x | the partner lane's x (quad_perm [1,0,3,2])
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    const uint32_t plo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0xB1, 0xF, 0xF, false);
+    const uint32_t phi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0xB1, 0xF, 0xF, false);
+    return x | ((uint64_t)phi << 32 | plo);
+}
+template <int N>
+__device__ __forceinline__ uint64_t legal_pair(uint64_t P, uint64_t O, const PairAxes& ax) {
+    constexpr uint64_t BD = Geo<N>::BOARD.w[0];
+    const uint64_t L = axis_var(P, O & ax.m0, ax.s0) | axis_var(P, O & ax.m1, ax.s1);
+    return pair_or(L) & ~(P | O) & BD;
+}
+// the side to move's possible_moves after a ply: one lane's whole scan, or the pair's split one
+template <int N, int RAYS>
+__device__ __forceinline__ uint64_t scan1(uint64_t P, uint64_t O, const PairAxes& ax) {
+    if constexpr (RAYS == RAYS_PAIR) {
+        return legal_pair<N>(P, O, ax);
+    } else {
+        uint64_t t[8];  // (the fills are not used: the flips come from the rays)
+        return OneWord<N>::legal(P, O, t);
+    }
+}
+
 // OthelloBaseEnv.step (othello.py:412-462) on a one-word board held as
 // (black B, white Wt, possible_moves L, meta m): step_lane + finish_step's
 // decisions, branch-free except the pass re-scan (taken by the wave only when
 // one of its lanes passes).  valid: the action is in possible_moves (`a` in
 // [0, N*N) then).  Returns reward / done / winner (0 unless the game ended).
+// RAYS_PAIR: lane h of a pair holding the same board (the flips and the
+// legal scans split over the pair; every result is the same on both lanes).
 template <int N, int RAYS = RAYS_MATH>
 __device__ __forceinline__ void step1(uint64_t& B, uint64_t& Wt, uint64_t& L, uint32_t& m, int a, bool valid,
                                       uint32_t flags, const uint64_t* __restrict__ rays, int& reward, int& done,
@@ -165,10 +225,10 @@ __device__ __forceinline__ void step1(uint64_t& B, uint64_t& Wt, uint64_t& L, ui
     const bool full = (P | O) == BD;                                        // :425-426
     const bool sudden = !valid && (flags & OTH_SUDDEN_DEATH);              // :427
     const bool stale = sudden || full;  // :431-433: turn and possible_moves stay as they were
-    uint64_t t[8];
-    uint64_t nl = OneWord<N>::legal(O, P, t);                               // :436
+    const PairAxes ax = pair_axes<N>(h);
+    uint64_t nl = scan1<N, RAYS>(O, P, ax);                                 // :436
     const bool opp_pass = nl == 0;
-    if (opp_pass && !stale) nl = OneWord<N>::legal(P, O, t);                // :437-440
+    if (opp_pass && !stale) nl = scan1<N, RAYS>(P, O, ax);                  // :437-440
     const bool term = stale || (opp_pass && nl == 0);                       // :441-442
     const int pc = popc64(P), oc = popc64(O);
     const int cur = tw ? WHITE_DISK : BLACK_DISK;
@@ -187,7 +247,11 @@ __device__ __forceinline__ void step1(uint64_t& B, uint64_t& Wt, uint64_t& L, ui
     m = (m & 0xff00u) | (new_tw ? M_TURN_WHITE : 0u) | (term ? M_TERMINATED | (wcode << M_WINNER_SHIFT) : 0u);
 }
 
-// One ply of every board, one lane per board.  More boards per lane (all
+// One ply of every board, one lane per board.  A lane pair per board (the
+// flips and the legal scans split over the pair as in k_sample_step2: twice
+// the waves, each lane's stream shorter) measured slower at 65,536 boards:
+// oth_step 2.94 -> 3.22 us per graphed ply, one random ply 3.24 -> 3.66
+// (profiles/r04/a/ab_ply.jsonl).  More boards per lane (all
 // their loads issued first, each group stepped as its own loads return, the
 // stores after the last group) measured slower at 262,144 and 1,048,576 boards
 // (2 per lane +2-6 %, 4 per lane +5-17 %), and so did a grid-stride loop with
@@ -313,10 +377,12 @@ __global__ __launch_bounds__(BLOCK) void k_ply_rand(uint64_t* __restrict__ board
     ply_body<N, PLY_RANDOM, RAYS>(boards, meta, legal, E, flags, actions, rewards, dones, wdl, rays, rng, ply);
 }
 
-// oth_create: the handle's ray table (fill_rays<N, true>'s layout) in device memory
+// oth_create: the handle's tables in device memory: the ray table (fill_rays<N,
+// true>'s 8 x 64 words) and the sel8 table (256 words, sel8_word) after it
 template <int N>
 __global__ __launch_bounds__(BLOCK) void k_fill_rays(uint64_t* __restrict__ rays) {
     fill_rays<N, true, false>(rays);
+    for (int i = threadIdx.x; i < 256; i += BLOCK) rays[8 * 64 + i] = sel8_word((uint32_t)i);
 }
 
 }  // namespace oth_dev

@@ -16,8 +16,10 @@ from . import _lib as L
 from .masked import _rows
 
 _OBS_LAYOUTS = {"board": L.OTH_OBS_BOARD, "board_legal": L.OTH_OBS_BOARD_LEGAL,
-                "make_state": L.OTH_OBS_MAKE_STATE, "absolute": L.OTH_OBS_ABSOLUTE}
-_OBS_PLANES = {L.OTH_OBS_BOARD: 1, L.OTH_OBS_BOARD_LEGAL: 2, L.OTH_OBS_MAKE_STATE: 4, L.OTH_OBS_ABSOLUTE: 1}
+                "make_state": L.OTH_OBS_MAKE_STATE, "absolute": L.OTH_OBS_ABSOLUTE, "legal": L.OTH_OBS_LEGAL}
+_OBS_PLANES = {L.OTH_OBS_BOARD: 1, L.OTH_OBS_BOARD_LEGAL: 2, L.OTH_OBS_MAKE_STATE: 4, L.OTH_OBS_ABSOLUTE: 1,
+               L.OTH_OBS_LEGAL: 1}
+_ONE_PLANE = (L.OTH_OBS_BOARD, L.OTH_OBS_ABSOLUTE, L.OTH_OBS_LEGAL)
 _DTYPES = {torch.int8: L.OTH_I8, torch.int32: L.OTH_I32, torch.int64: L.OTH_I64,
            torch.float32: L.OTH_F32, torch.float64: L.OTH_F64}
 _POLICIES = {"random": L.OTH_POLICY_RANDOM, "greedy": L.OTH_POLICY_GREEDY}
@@ -75,6 +77,10 @@ class VecOthelloEnv(object):
                                          self.env_id_base, self.initial_rand_steps, self.device.index,
                                          ctypes.byref(h)), "oth_create")
         self._h = h
+        self._hv = h.value  # the handle as an int: the per-step ctypes calls take it as is
+        self._dev_index = self.device.index
+        self._step_fn = self._lib.oth_step
+        self._bview = None  # (dones tensor, its bool view): step()'s view of caller-given dones, cached
         self._sample_calls = 0  # Philox counter of sample_actions
         self._region_resets = None  # resets inside an open graph region (None: no region)
 
@@ -88,6 +94,7 @@ class VecOthelloEnv(object):
         if getattr(self, "_h", None):
             self._lib.oth_destroy(self._h)
             self._h = None
+            self._hv = None  # a later step() passes NULL: OTH_EINVAL, not a freed handle
 
     def __del__(self):
         try:
@@ -138,16 +145,27 @@ class VecOthelloEnv(object):
     def step(self, actions, rewards=None, dones=None, observe=True):
         """OthelloBaseEnv.step (othello.py:412-462) on every board.
 
-        actions: int tensor (E,).  Returns (obs, rewards int32 (E,), dones bool (E,), None)
-        -- obs is None when observe=False."""
-        a = actions.to(device=self.device, dtype=torch.int32).contiguous()
+        actions: int tensor (E,).  rewards / dones: optional int32 / uint8 (E,)
+        tensors on this device, written in place (the loop form: no allocation
+        per step).  Returns (obs, rewards int32 (E,), dones bool (E,), None) --
+        obs is None when observe=False.  The host path is one ctypes call: an
+        int32 contiguous action tensor on this device is passed as is."""
+        a = actions
+        if a.dtype is not torch.int32 or not a.is_contiguous() or a.device != self.device:
+            a = a.to(device=self.device, dtype=torch.int32).contiguous()
         if a.numel() != self.num_envs:
             raise ValueError("expected %d actions, got %d" % (self.num_envs, a.numel()))
         r = rewards if rewards is not None else self._i32(self.num_envs)
         d = dones if dones is not None else self._u8(self.num_envs)
-        L.check(self._lib.oth_step(self._h, _ptr(a), _ptr(r), _ptr(d), self._stream()), "oth_step")
+        st = _RAW_STREAM(self._dev_index) if _RAW_STREAM is not None else self._stream()
+        rc = self._step_fn(self._hv, a.data_ptr(), r.data_ptr(), d.data_ptr(), st)
+        if rc:
+            L.check(rc, "oth_step")
         obs = self.get_observation() if observe else None
-        return obs, r, d.view(torch.bool), None  # 0/1 bytes: a view, not a conversion kernel
+        bv = self._bview
+        if bv is None or bv[0] is not d:  # 0/1 bytes: a view, not a conversion kernel
+            bv = self._bview = (d, d.view(torch.bool))
+        return obs, r, bv[1], None
 
     def step_policy(self, policy="random", n_plies=1, actions=None, rewards=None, dones=None, record=True):
         """n_plies plies where every board's mover plays `policy` on the device
@@ -206,9 +224,10 @@ class VecOthelloEnv(object):
         return out
 
     def legal_actions(self):
-        """possible_moves as a bool (E, N*N) tensor (the obs legal plane, unconditioned)."""
-        o = self.observe("board_legal", torch.int8)
-        return o[:, 1].reshape(self.num_envs, -1).bool()
+        """possible_moves as a bool (E, N*N) tensor: the OTH_OBS_LEGAL plane in int8,
+        viewed as bool (one kernel writing E*N*N bytes, no conversion)."""
+        o = self.observe("legal", torch.int8)
+        return o.view(torch.bool).reshape(self.num_envs, -1)
 
     def greedy_actions(self):
         """GreedyPolicy.get_action (simple_policies.py:69-92) for every board."""
@@ -226,8 +245,7 @@ class VecOthelloEnv(object):
         lay = _OBS_LAYOUTS[layout] if isinstance(layout, str) else int(layout)
         planes = _OBS_PLANES[lay]
         n = self.board_size
-        shape = (self.num_envs, n, n) if lay in (L.OTH_OBS_BOARD, L.OTH_OBS_ABSOLUTE) else \
-            (self.num_envs, planes, n, n)
+        shape = (self.num_envs, n, n) if lay in _ONE_PLANE else (self.num_envs, planes, n, n)
         if out is None:
             out = torch.empty(shape, dtype=dtype, device=self.device)
         L.check(self._lib.oth_observe(self._h, lay, _DTYPES[out.dtype], _ptr(out), self._stream()),

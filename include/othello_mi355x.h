@@ -73,7 +73,9 @@ enum {
     OTH_OBS_BOARD = 0,       /* (E,N,N)   get_observation(): mover +1, opponent -1 (othello.py:363-369) */
     OTH_OBS_BOARD_LEGAL = 1, /* (E,2,N,N) get_observation() with possible_actions_in_obs (othello.py:370-376) */
     OTH_OBS_MAKE_STATE = 2,  /* (E,4,N,N) util.make_state(obs, env) planes (util.py:48-74) */
-    OTH_OBS_ABSOLUTE = 3     /* (E,N,N)   board_state: white +1, black -1 (othello.py:257) */
+    OTH_OBS_ABSOLUTE = 3,    /* (E,N,N)   board_state: white +1, black -1 (othello.py:257) */
+    OTH_OBS_LEGAL = 4        /* (E,N,N)   possible_moves as 0 / 1 (othello.py:313-343; the plane of
+                                          OTH_OBS_BOARD_LEGAL alone: int8 views as a bool mask) */
 };
 /* observation element types */
 enum { OTH_I8 = 0, OTH_I32 = 1, OTH_I64 = 2, OTH_F32 = 3, OTH_F64 = 4 };

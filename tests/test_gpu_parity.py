@@ -526,6 +526,8 @@ def _obs_np(n, boards, meta, legal, layout):
     E = len(meta)
     if layout == "absolute":
         return (w - b).reshape(E, n, n)
+    if layout == "legal":
+        return lg.reshape(E, n, n)
     mover = np.where(tw, w - b, b - w)
     if layout == "board":
         return mover.reshape(E, n, n)
@@ -545,7 +547,7 @@ def test_observation_kernels_every_layout_and_alignment(torch_cuda, n):
     env = make_env(torch, E, n, auto=True, seed=5)
     env.step_policy("random", n_plies=n * n // 2 + 3, record=False)
     b, m, lg = get_state_np(env)
-    for layout in ("board", "board_legal", "make_state", "absolute"):
+    for layout in ("board", "board_legal", "make_state", "absolute", "legal"):
         want = _obs_np(n, b, m, lg, layout)
         for dt in (torch.int8, torch.int32, torch.int64, torch.float32, torch.float64):
             got = env.observe(layout, dt)
@@ -554,6 +556,22 @@ def test_observation_kernels_every_layout_and_alignment(torch_cuda, n):
             off = buf[1:].view(want.shape)  # base one element past the vector alignment
             env.observe(layout, dt, out=off)
             np.testing.assert_array_equal(off.cpu().numpy(), want, err_msg="unaligned %s %s" % (layout, dt))
+    np.testing.assert_array_equal(env.legal_actions().cpu().numpy(),
+                                  _obs_np(n, b, m, lg, "legal").reshape(E, n * n).astype(bool))
+
+
+@pytest.mark.parametrize("n,E", [(8, 65536), (8, 262144), (6, 100003), (10, 70000)])
+def test_observation_kernels_at_size(torch_cuda, n, E):
+    """k_observe_w's two wave shapes (16 boards per wave below 262,144 boards,
+    64 from there) at the configs' sizes and ragged E: int64 BOARD and f32
+    MAKE_STATE equal the numpy restatement."""
+    torch = torch_cuda
+    env = make_env(torch, E, n, auto=True, seed=8)
+    env.step_policy("random", n_plies=n * n // 2 + 1, record=False)
+    b, m, lg = get_state_np(env)
+    for layout, dt in (("board", torch.int64), ("make_state", torch.float32), ("legal", torch.int8)):
+        np.testing.assert_array_equal(env.observe(layout, dt).cpu().numpy(), _obs_np(n, b, m, lg, layout),
+                                      err_msg="%s %s" % (layout, dt))
 
 
 @pytest.mark.parametrize("n,opp", [(8, "random"), (6, "greedy")])

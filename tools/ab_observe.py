@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of compile-time variants of the observation encoders
+(k_observe_w) in ONE process: int64 BOARD and f32 MAKE_STATE into preallocated
+tensors, each variant's launches captured in a HIP graph and replayed; every
+variant must write the same values (checked first).
+
+    python tools/ab_variants.py --build old=-DOTH_OBS_SMALL_E=0 new=       # here (CPU, hipcc)
+    python tools/ab_observe.py old new [--envs 65536,1048576 --launches 50 --rounds 6]   # GPU box
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+VDIR = os.path.join(ROOT, "gymothelloenv_amd", "variants")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("names", nargs="+")
+    ap.add_argument("--envs", default="65536,1048576")
+    ap.add_argument("--board-size", type=int, default=8)
+    ap.add_argument("--launches", type=int, default=50)
+    ap.add_argument("--rounds", type=int, default=6)
+    a = ap.parse_args()
+    import torch
+
+    import bench
+    from gymothelloenv_amd import _lib as L
+    from gymothelloenv_amd.vec_env import VecOthelloEnv
+    dev = torch.device("cuda", 0)
+    libs = {nm: L.load_path(os.path.join(VDIR, "liboth_%s.so" % nm)) for nm in a.names}
+    n = a.board_size
+    for E in [int(x) for x in a.envs.split(",")]:
+        envs = {nm: VecOthelloEnv(E, board_size=n, auto_reset=True, seed=3, device=dev, lib=lib)
+                for nm, lib in libs.items()}
+        for env in envs.values():
+            env.step_policy("random", n_plies=25, record=False)
+        for layout, dt, esize in (("board", torch.int64, 8), ("make_state", torch.float32, 4)):
+            shape = (E, n, n) if layout == "board" else (E, 4, n, n)
+            bufs = {nm: torch.empty(shape, dtype=dt, device=dev) for nm in a.names}
+            ref = None
+            for nm, env in envs.items():
+                env.observe(layout, dt, out=bufs[nm])
+                if ref is None:
+                    ref = bufs[nm].clone()
+                assert torch.equal(bufs[nm], ref), "variant %s writes other values" % nm
+            graphs = {}
+            for nm, env in envs.items():
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    for _ in range(a.launches):
+                        env.observe(layout, dt, out=bufs[nm])
+                graphs[nm] = g
+            times = {nm: [] for nm in a.names}
+            for r in range(a.rounds + 1):
+                for nm in a.names:
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    torch.cuda.synchronize()
+                    e0.record()
+                    graphs[nm].replay()
+                    e1.record()
+                    torch.cuda.synchronize()
+                    if r:
+                        times[nm].append(e0.elapsed_time(e1) * 1e3 / a.launches)
+            b = bench.observe_bytes(n, E, layout, esize)
+            res = {nm: {"us": statistics.median(t), "GBps": b / (statistics.median(t) * 1e-6) / 1e9}
+                   for nm, t in times.items()}
+            print(json.dumps({"E": E, "layout": layout, "dtype": str(dt), "bytes": b, "results": res}), flush=True)
+            del graphs, bufs
+
+
+if __name__ == "__main__":
+    main()

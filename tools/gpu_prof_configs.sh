@@ -3,9 +3,9 @@
 # Usage: bash tools/gpu_prof_configs.sh <outdir> [case groups, e.g. greedy10 greedy100 rand6,rand10 obs]
 set -o pipefail
 O=${1:-gpurun_out/r04cfg}; shift || true
-GROUPS=${@:-"greedy10 greedy100 rand6,rand10 obs"}
+CASES=${@:-"greedy10 greedy100 rand6,rand10 obs"}
 export TMPDIR=/tmp
-for G in $GROUPS; do
+for G in $CASES; do
   D=$O/$(echo $G | tr ',' '_')
   mkdir -p $D
   timeout -k 10 200 python3 tools/prof_configs.py --cases $G > $D/times.jsonl 2> $D/times.err || { tail $D/times.err; exit 1; }
