@@ -935,26 +935,13 @@ struct OneWord {
         run_len<-N>(t[5], n[5]);
         run_len<-N - 1>(t[6], n[6]);
         run_len<-N + 1>(t[7], n[7]);
-#ifndef OTH_GREEDY_AXIS_SUM
-#define OTH_GREEDY_AXIS_SUM 1  // A/B of round 4 (0: round 3's pairing, 4-bit first sums)
-#endif
-        uint64_t tot[5];
-        if constexpr (OTH_GREEDY_AXIS_SUM) {
-            static_assert(N - 2 <= 7, "an axis' two runs fit 3 bits");
-            uint64_t s3[4][3], s4[2][4];
+        static_assert(N - 2 <= 7, "an axis' two runs fit 3 bits");
+        uint64_t s3[4][3], s4[2][4], tot[5];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) add_planes<3, 3, 3>(n[i], n[i + 4], s3[i]);  // d and its opposite d + 4
-            add_planes<3, 3, 4>(s3[0], s3[1], s4[0]);
-            add_planes<3, 3, 4>(s3[2], s3[3], s4[1]);
-            add_planes<4, 4, 5>(s4[0], s4[1], tot);
-        } else {
-            uint64_t s4[4][4], s5[2][5];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) add_planes<3, 3, 4>(n[2 * i], n[2 * i + 1], s4[i]);
-            add_planes<4, 4, 5>(s4[0], s4[1], s5[0]);
-            add_planes<4, 4, 5>(s4[2], s4[3], s5[1]);
-            add_planes<5, 5, 5>(s5[0], s5[1], tot);
-        }
+        for (int i = 0; i < 4; ++i) add_planes<3, 3, 3>(n[i], n[i + 4], s3[i]);  // d and its opposite d + 4
+        add_planes<3, 3, 4>(s3[0], s3[1], s4[0]);
+        add_planes<3, 3, 4>(s3[2], s3[3], s4[1]);
+        add_planes<4, 4, 5>(s4[0], s4[1], tot);
         uint64_t cand = legal;
 #pragma unroll
         for (int i = 4; i >= 0; --i) {

@@ -973,6 +973,7 @@ __global__ __launch_bounds__(BLOCK) void k_play(uint64_t* __restrict__ boards, u
 struct NoFill {
     __device__ __forceinline__ void operator()() const {}
 };
+
 // black wins / draws / white wins from play_rand_fast's (sum of black's signs, games, decided games)
 __device__ __forceinline__ void tally_from_signs(uint32_t s, uint32_t g, uint32_t z, uint32_t& cb, uint32_t& cd,
                                                  uint32_t& cw) {
@@ -1063,11 +1064,10 @@ __device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_
     }
 }
 
-#ifndef OTH_PLAY_TABLES
-#define OTH_PLAY_TABLES 1  // A/B of round 4: k_play_rand's LDS tables copied from the handle's (0: built per block)
-#endif
 // tables: the handle's ray + sel8 tables (oth_env::rays, k_fill_rays), copied into
 // LDS by one 16-byte and one 8-byte load per thread, issued with the board's loads
+// (against building them per block: greedy 10-ply launches 1.85 -> 1.80 us per
+// ply, random 100-ply 0.679 -> 0.678; profiles/r04/b/)
 template <int N, int POLICY = OTH_POLICY_RANDOM>
 __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
                                                      uint64_t* __restrict__ legal, int E, uint32_t flags, int plies,
@@ -1083,19 +1083,12 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
     const uint8_t* sel8 = reinterpret_cast<const uint8_t*>(lds_sel);
     const int e = blockIdx.x * BLOCK + threadIdx.x;
     Lane<N> s;
-#if OTH_PLAY_TABLES
     const ulonglong2 tr = reinterpret_cast<const ulonglong2*>(tables)[threadIdx.x];
     const uint64_t ts = tables[Fills<N>::RAY_WORDS + threadIdx.x];
     if (e < E) load_lane<N>(s, boards, meta, legal, e);
     reinterpret_cast<ulonglong2*>(lds_rays)[threadIdx.x] = tr;
     lds_sel[threadIdx.x] = ts;
     __syncthreads();
-#else
-    for (int i = threadIdx.x; i < 256; i += BLOCK) lds_sel[i] = sel8_word((uint32_t)i);
-    fill_rays<N, turned_rays<Fills<N>>::value>(lds_rays);  // (its barrier covers lds_sel)
-    (void)tables;
-    if (e < E) load_lane<N>(s, boards, meta, legal, e);
-#endif
     uint32_t cb = 0, cd = 0, cw = 0;
     if (e < E) {
         const uint32_t id = rng.id_base + (uint32_t)e;
@@ -1124,7 +1117,10 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
             play_rand_fast<N, POLICY, OPEN>(M, O, L, mt, eng, u, flags, rng, id, ply0 + (uint64_t)p, a, r, d, t0, t1,
                                             t2, fill, sel8);
             // the trajectory rows are written once: streaming stores (+0.9 % at 65,536
-            // boards, +0.7 % at 131,072; profiles/r03/nt/)
+            // boards, +0.7 % at 131,072; profiles/r03/nt/).  Row stores at a scalar
+            // (SGPR) row base and a constant lane offset -- 3 VALU fewer per ply, 32 SALU
+            // more per 4-ply group -- measured 0.674 -> 0.709 us per ply (the lone wave's
+            // issue slots: profiles/r04/c/ab_saddr.jsonl), so the running pointers stay
             __builtin_nontemporal_store(a, act_p);
             __builtin_nontemporal_store(r, rew_p);
             __builtin_nontemporal_store((uint8_t)d, done_p);
@@ -1134,12 +1130,7 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
         };
         const NoFill nofill;
         if constexpr (POLICY != OTH_POLICY_RANDOM) {  // scripted policy: draws only on opening plies
-#ifndef OTH_OPEN_BLOCK
-#define OTH_OPEN_BLOCK 1  // A/B of round 4 (0: round 3's Philox evaluation per opening ply)
-#endif
-            if constexpr (OPEN && !OTH_OPEN_BLOCK) {
-                for (int p = 0; p < plies; ++p) ply(p, action_draw(rng.seed, id, ply0 + (uint64_t)p), nofill);
-            } else if constexpr (OPEN) {
+            if constexpr (OPEN) {
                 // an opening ply's draw is word g % 4 of Philox block g / 4 (action_draw's
                 // value); the block is computed once per group of four plies, at the first
                 // ply where some board of the wave has opening plies left (uniform branch):

@@ -254,11 +254,11 @@ int launch_legal_moves(int n, const uint64_t* mover, const uint64_t* opp, uint64
     return after_launch("oth_legal_moves");
 }
 
+// observations of fewer boards: 16 boards per wave (k_observe_w; make_state f32 at
+// 65,536 boards 29.3 -> 13.8 us, int64 board 9.9 -> 9.6; 8 or 4 boards per wave:
+// 13.1 / 13.2 and 9.7 / 9.9 us, profiles/r04/b/ab_obs.jsonl)
 #ifndef OTH_OBS_SMALL_E
-#define OTH_OBS_SMALL_E 262144  // observations of fewer boards: OTH_OBS_BPW boards per wave (k_observe_w)
-#endif
-#ifndef OTH_OBS_BPW
-#define OTH_OBS_BPW 16
+#define OTH_OBS_SMALL_E 262144
 #endif
 
 // one wave per BPW boards (k_observe_w), vector stores of 4 squares: N*N % 4 == 0
@@ -291,7 +291,7 @@ void launch_observe_bpw(oth_env* env, int layout, T* o, hipStream_t st) {
 template <int N, typename T>
 void launch_observe_w(oth_env* env, int layout, void* out, hipStream_t st) {
     T* o = static_cast<T*>(out);
-    if (env->E < OTH_OBS_SMALL_E) launch_observe_bpw<N, T, OTH_OBS_BPW>(env, layout, o, st);
+    if (env->E < OTH_OBS_SMALL_E) launch_observe_bpw<N, T, 16>(env, layout, o, st);
     else launch_observe_bpw<N, T, 64>(env, layout, o, st);
 }
 
