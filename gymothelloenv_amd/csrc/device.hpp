@@ -1652,10 +1652,8 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const uint64_t* __restrict__ 
 
 // A quad of 4 consecutive squares of one plane as one vector store (16 B for
 // f32 / i32, 4 B for i8, 2 x 16 B for the 8-byte types): k_observe_w's unit.
-template <typename T>
-struct Quad {
-    T v[4];
-};
+// (as streaming stores: 65,536 boards 2-3 % slower, 1,048,576 int64 boards 104 -> 250 us;
+// profiles/r04/d/ab_obs_nt.jsonl)
 template <typename T>
 __device__ __forceinline__ void put_quad(T* out, uint32_t q, int v0, int v1, int v2, int v3) {
     if constexpr (sizeof(T) == 1) {

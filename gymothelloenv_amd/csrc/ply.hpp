@@ -343,7 +343,7 @@ __device__ __forceinline__ void ply_body(uint64_t* __restrict__ boards, uint16_t
         }
         if constexpr (SRC == PLY_RANDOM)
             if (actions) actions[e] = a;
-        if (NT) {
+        if (NT) {  // (dones, half a line a wave, through L2 instead: +-0 at 1,048,576; profiles/r04/d/)
             if (rewards) __builtin_nontemporal_store(r, &rewards[e]);
             if (dones) __builtin_nontemporal_store((uint8_t)d, &dones[e]);
         } else {

@@ -2,6 +2,7 @@
 """Summarise tools/pmc_profile.sh output into profiles/pmc_traffic.json.
 
     python tools/pmc_summarize.py gpurun_out/pmc1 random-play-8x8-E65536-P100
+    python tools/pmc_summarize.py DIR WORKLOAD --kernel "k_play_rand<8, 1>" --out pmc_configs.json
 
 Per dispatch of the bench kernel (k_play): FETCH_SIZE / WRITE_SIZE (KiB, from
 separate passes) -> HBM bytes, with the gfx950 correction of
@@ -42,8 +43,15 @@ def trace_avg(path, kernel="k_play"):
 
 
 def main():
-    path, workload = sys.argv[1], sys.argv[2]
-    c, dur = per_dispatch(path)
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("path")
+    ap.add_argument("workload")
+    ap.add_argument("--kernel", default="k_play", help="substring of the kernel name (first match)")
+    ap.add_argument("--out", default="pmc_traffic.json", help="file under profiles/")
+    a = ap.parse_args()
+    path, workload = a.path, a.workload
+    c, dur = per_dispatch(path, a.kernel)
     fetch = c.get("FETCH_SIZE", 0.0) * 1024
     write = c.get("WRITE_SIZE", 0.0) * 1024
     rec = {
@@ -60,10 +68,10 @@ def main():
         "active_inst_any_quad": c.get("SQ_ACTIVE_INST_ANY"),
         "grbm_gui_active": c.get("GRBM_GUI_ACTIVE"),
         "profiled_dispatch_avg_ns": dur,
-        "kernel_trace": trace_avg(path),
+        "kernel_trace": trace_avg(path, a.kernel),
         "source": os.path.relpath(path, ROOT),
     }
-    out = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    out = os.path.join(ROOT, "profiles", a.out)
     d = json.load(open(out)) if os.path.exists(out) else {}
     d[workload] = rec
     json.dump(d, open(out, "w"), indent=1, sort_keys=True)
