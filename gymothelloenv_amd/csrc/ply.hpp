@@ -247,7 +247,12 @@ __device__ __forceinline__ void step1(uint64_t& B, uint64_t& Wt, uint64_t& L, ui
     m = (m & 0xff00u) | (new_tw ? M_TURN_WHITE : 0u) | (term ? M_TERMINATED | (wcode << M_WINNER_SHIFT) : 0u);
 }
 
-// One ply of every board, one lane per board.  A lane pair per board (the
+// One ply of every board, one lane per board, 256 threads per block (128 or 64:
+// ±0 to +4 % at 65,536 and 1,048,576 boards, also with computed rays at every
+// size; profiles/r04/e/ab_block.jsonl).  Two boards per lane (the second
+// board's loads in flight while the first is stepped and stored) measured
+// slower again in round 4: 262,144 boards 5.79 -> 6.14 us per ply, 1,048,576
+// 12.82 -> 13.33 (profiles/r04/f/ab_bpl2.jsonl).  A lane pair per board (the
 // flips and the legal scans split over the pair as in k_sample_step2: twice
 // the waves, each lane's stream shorter) measured slower at 65,536 boards:
 // oth_step 2.94 -> 3.22 us per graphed ply, one random ply 3.24 -> 3.66
