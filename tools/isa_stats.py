@@ -32,7 +32,7 @@ def kernels(asm):
         meta[m.group(1)] = (int(m.group(2)), int(m.group(3)))
     for m in re.finditer(r"^(_Z\S+):\s*;.*$", asm, re.M):
         name = m.group(1)
-        end = asm.find("s_endpgm", m.end())
+        end = asm.find(".Lfunc_end", m.end())  # the whole body: block placement may put an s_endpgm mid-function
         body = asm[m.end():end]
         ins = re.findall(r"^\s+([a-z_][a-z0-9_]*)", body, re.M)
         res[name] = (ins, body, meta.get(name))
