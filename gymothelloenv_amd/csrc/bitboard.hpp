@@ -115,9 +115,22 @@ OTH_HD bool test(const BB<W>& b, int a) {
 
 OTH_HD int popc64(uint64_t x) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    return __popcll(x);
+    // two 32-bit counts (one v_bcnt_u32_b32 chain) as an i32: compares of counts
+    // stay 32-bit (__popcll's i64 count put 64-bit compares into the select)
+    return __popc((uint32_t)x) + __popc((uint32_t)(x >> 32));
 #else
     return __builtin_popcountll(x);
+#endif
+}
+// -1, 0 or +1: one v_med3_i32 on the device (LLVM turns min(max(x, -1), 1) of a
+// difference into two compares and two selects)
+OTH_HD int sign_i32(int x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    int r;
+    asm("v_med3_i32 %0, %1, -1, 1" : "=v"(r) : "v"(x));
+    return r;
+#else
+    return x > 0 ? 1 : (x < 0 ? -1 : 0);
 #endif
 }
 OTH_HD int ctz64(uint64_t x) {  // x != 0

@@ -1013,54 +1013,114 @@ __device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_
     const uint64_t f = eng.flip(dummy, dummy, a).w[0];  // update_board (othello.py:391-410)
     const uint64_t Mn = M | f | m, On = O & ~f;
     const bool full = (Mn | On) == BD;  // :425-426
-    BB<1> pb, ob;
-    pb.w[0] = On;
-    ob.w[0] = Mn;
-    uint64_t Ln = eng.legal(pb, ob).w[0];  // the opponent's possible_moves (:436), fills kept in eng.t
-    fill();
-    const bool pass = Ln == 0 && !full;
-    if (pass) {  // :437-440: the mover moves again (fills recomputed for the mover)
-        pb.w[0] = Mn;
-        ob.w[0] = On;
-        Ln = eng.legal(pb, ob).w[0];
-    }
-    const bool term = full || Ln == 0;  // full board or nobody can move (:441-442)
-    // (M, O) := (next mover, its opponent).  Alternating the two words' roles
-    // statically from ply to ply instead (no selects; a pass swapping them in its
-    // own exec-masked block) measured 2.3 % slower; per-ply outputs through buffer descriptors (no 64-bit
-    // address VALU) 2.3 % slower too, their descriptor SALU in the same issue stream
-    // (profiles/r03/st/)
-    const bool swap = !pass && !full;
-    M = swap ? On : Mn;
-    O = swap ? Mn : On;
-    L = Ln;
-    meta ^= swap ? M_TURN_WHITE : 0u;
-    r = 0;
-    d = term ? 1 : 0;
-    if (term) {
-        const int pc = popc64(Mn), oc = popc64(On), df = pc - oc;
-        const int sg = min(max(df, -1), 1);  // v_med3_i32: the mover's result
-        if (flags & OTH_DISK_REWARD) r = oc == 0 ? NN : df;  // :446-459
-        else r = sg;                                           // winner * player_turn
-        // the tally as (cb, cd, cw) = (sum of black's signs, games, decided games),
-        // turned into wins / draws / wins by tally_from_signs: three adds, no selects
-        const int m = -(int)(meta & M_TURN_WHITE);  // the mover (the turn is not passed on): 0 black, -1 white
-        const int sb = (sg ^ m) - m;                // black's result
-        cb += (uint32_t)sb;
-        cd += 1u;
-        cw += (uint32_t)__mul24(sb, sb);
-        // auto-reset (othello.py:256-271): black to move from the start position
-        M = Start<N>::BLACK.w[0];
-        O = Start<N>::WHITE.w[0];
-        constexpr uint64_t START_MOVES = start_moves<N>();  // constant-evaluated
-        constexpr StartFills<N> SF = start_fills<N>();
-        L = START_MOVES;
+    if constexpr (POLICY == OTH_POLICY_RANDOM) {
+        // random play: a full board ends the game and auto-resets (othello.py:256-271)
+        // before the scan, which then runs on the start position (black to move)
+        // instead of the full board, where it would find nothing: the reset's
+        // possible_moves and fills come from it and the terminal block holds no reset
+        // moves; only a double pass (inside the pass block) resets explicitly.  8x8
+        // 0.678 -> 0.675 us per ply, 6x6 -1.6 %; for greedy play it measured 3 % slower
+        // (the scan waits on the full-board select), so greedy keeps the reset in the
+        // terminal block (profiles/r04/g/ab_term.jsonl)
+        constexpr uint64_t B0 = Start<N>::BLACK.w[0], W0 = Start<N>::WHITE.w[0];
+        BB<1> pb, ob;
+        pb.w[0] = full ? B0 : On;
+        ob.w[0] = full ? W0 : Mn;
+        uint64_t Ln = eng.legal(pb, ob).w[0];  // the next mover's possible_moves (:436), fills kept in eng.t
+        fill();
+        const bool pass = Ln == 0;  // never on the start position
+        bool term = full;
+        M = pb.w[0];
+        O = ob.w[0];
+        if (pass) {  // :437-440: the mover moves again (fills recomputed for the mover)
+            pb.w[0] = Mn;
+            ob.w[0] = On;
+            Ln = eng.legal(pb, ob).w[0];
+            M = Mn;
+            O = On;
+            if (Ln == 0) {  // nobody can move (:441-442): reset
+                term = true;
+                M = B0;
+                O = W0;
+                constexpr uint64_t START_MOVES = start_moves<N>();
+                constexpr StartFills<N> SF = start_fills<N>();
+                Ln = START_MOVES;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) eng.t[k] = SF.t[k];
-        uint32_t rl = 0;
-        if (rng.init_rand > 0)
-            rl = (uint32_t)scale_index(philox_x(rng.seed, id, g, RNG_OPENING_AUTO), rng.init_rand / 2 + 1) * 2u;
-        meta = (rl & 0xffu) << M_RAND_SHIFT;
+                for (int k = 0; k < 8; ++k) eng.t[k] = SF.t[k];
+            }
+        }
+        L = Ln;
+        const uint32_t mover = meta;
+        meta ^= pass ? 0u : M_TURN_WHITE;
+        r = 0;
+        d = term ? 1 : 0;
+        if (term) {
+            const int pc = popc64(Mn), oc = popc64(On), df = pc - oc;
+            const int sg = sign_i32(df);  // the mover's result
+            if (flags & OTH_DISK_REWARD) r = oc == 0 ? NN : df;  // :446-459
+            else r = sg;                                           // winner * player_turn
+            // the tally as (cb, cd, cw) = (sum of black's signs, games, decided games),
+            // turned into wins / draws / wins by tally_from_signs: three adds, no selects
+            const int mw = -(int)(mover & M_TURN_WHITE);  // 0 black, -1 white
+            const int sb = (sg ^ mw) - mw;                // black's result
+            cb += (uint32_t)sb;
+            cd += 1u;
+            cw += (uint32_t)__mul24(sb, sb);
+            uint32_t rl = 0;
+            if (rng.init_rand > 0)
+                rl = (uint32_t)scale_index(philox_x(rng.seed, id, g, RNG_OPENING_AUTO), rng.init_rand / 2 + 1) * 2u;
+            meta = (rl & 0xffu) << M_RAND_SHIFT;
+        }
+    } else {
+        BB<1> pb, ob;
+        pb.w[0] = On;
+        ob.w[0] = Mn;
+        uint64_t Ln = eng.legal(pb, ob).w[0];  // the opponent's possible_moves (:436), fills kept in eng.t
+        fill();
+        const bool pass = Ln == 0 && !full;
+        if (pass) {  // :437-440: the mover moves again (fills recomputed for the mover)
+            pb.w[0] = Mn;
+            ob.w[0] = On;
+            Ln = eng.legal(pb, ob).w[0];
+        }
+        const bool term = full || Ln == 0;  // full board or nobody can move (:441-442)
+        // (M, O) := (next mover, its opponent).  Alternating the two words' roles
+        // statically from ply to ply instead (no selects; a pass swapping them in its
+        // own exec-masked block) measured 2.3 % slower; per-ply outputs through buffer descriptors (no 64-bit
+        // address VALU) 2.3 % slower too, their descriptor SALU in the same issue stream
+        // (profiles/r03/st/)
+        const bool swap = !pass && !full;
+        M = swap ? On : Mn;
+        O = swap ? Mn : On;
+        L = Ln;
+        meta ^= swap ? M_TURN_WHITE : 0u;
+        r = 0;
+        d = term ? 1 : 0;
+        if (term) {
+            const int pc = popc64(Mn), oc = popc64(On), df = pc - oc;
+            const int sg = sign_i32(df);  // the mover's result
+            if (flags & OTH_DISK_REWARD) r = oc == 0 ? NN : df;  // :446-459
+            else r = sg;                                           // winner * player_turn
+            // the tally as (cb, cd, cw) = (sum of black's signs, games, decided games),
+            // turned into wins / draws / wins by tally_from_signs: three adds, no selects
+            const int m = -(int)(meta & M_TURN_WHITE);  // the mover (the turn is not passed on): 0 black, -1 white
+            const int sb = (sg ^ m) - m;                // black's result
+            cb += (uint32_t)sb;
+            cd += 1u;
+            cw += (uint32_t)__mul24(sb, sb);
+            // auto-reset (othello.py:256-271): black to move from the start position
+            M = Start<N>::BLACK.w[0];
+            O = Start<N>::WHITE.w[0];
+            constexpr uint64_t START_MOVES = start_moves<N>();  // constant-evaluated
+            constexpr StartFills<N> SF = start_fills<N>();
+            L = START_MOVES;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) eng.t[k] = SF.t[k];
+            uint32_t rl = 0;
+            if (rng.init_rand > 0)
+                rl = (uint32_t)scale_index(philox_x(rng.seed, id, g, RNG_OPENING_AUTO), rng.init_rand / 2 + 1) * 2u;
+            meta = (rl & 0xffu) << M_RAND_SHIFT;
+        }
     }
 }
 
@@ -1238,34 +1298,47 @@ __device__ __forceinline__ void play_rand_fast_w(BB<Geo<N>::W>& M, BB<Geo<N>::W>
     const BB<W> f = eng.flip(M, O, a);  // update_board (othello.py:391-410)
     const BB<W> Mn = M | f | m, On = O & ~f;
     const bool full = !any(~(Mn | On) & Geo<N>::BOARD);  // :425-426
-    BB<W> Ln = eng.legal(On, Mn);                          // the opponent's possible_moves (:436)
-    fill();
-    const bool pass = !any(Ln) && !full;
-    if (pass) Ln = eng.legal(Mn, On);  // :437-440
-    const bool term = full || !any(Ln);
-    const bool swap = !pass && !full;
+    // a full board resets before the scan, as in play_rand_fast: the next mover's
+    // scan runs on the start position, and only a double pass scans it again
+    // (10x10: 1.692 -> 1.689 us per ply, profiles/r04/g/ab_term.jsonl)
+    BB<W> nM, nO;
 #pragma unroll
     for (int i = 0; i < W; ++i) {
-        M.w[i] = swap ? On.w[i] : Mn.w[i];
-        O.w[i] = swap ? Mn.w[i] : On.w[i];
+        nM.w[i] = full ? Start<N>::BLACK.w[i] : On.w[i];
+        nO.w[i] = full ? Start<N>::WHITE.w[i] : Mn.w[i];
+    }
+    BB<W> Ln = eng.legal(nM, nO);  // the next mover's possible_moves (:436)
+    fill();
+    const bool pass = !any(Ln);  // never on the start position
+    bool term = full;
+    M = nM;
+    O = nO;
+    if (pass) {  // :437-440
+        Ln = eng.legal(Mn, On);
+        M = Mn;
+        O = On;
+        if (!any(Ln)) {  // nobody can move (:441-442): reset
+            term = true;
+            M = Start<N>::BLACK;
+            O = Start<N>::WHITE;
+            Ln = eng.legal(M, O);
+        }
     }
     L = Ln;
-    meta ^= swap ? M_TURN_WHITE : 0u;
+    const uint32_t mover = meta;
+    meta ^= pass ? 0u : M_TURN_WHITE;
     r = 0;
     d = term ? 1 : 0;
     if (term) {
         const int pc = popcount(Mn), oc = popcount(On), df = pc - oc;
-        const int sg = min(max(df, -1), 1);  // the mover's result
+        const int sg = sign_i32(df);  // the mover's result
         if (flags & OTH_DISK_REWARD) r = oc == 0 ? NN : df;  // :446-459
         else r = sg;
-        const int mw = -(int)(meta & M_TURN_WHITE);  // (cb, cd, cw) as in play_rand_fast
+        const int mw = -(int)(mover & M_TURN_WHITE);  // (cb, cd, cw) as in play_rand_fast
         const int sb = (sg ^ mw) - mw;
         cb += (uint32_t)sb;
         cd += 1u;
         cw += (uint32_t)__mul24(sb, sb);
-        M = Start<N>::BLACK;  // auto-reset (othello.py:256-271)
-        O = Start<N>::WHITE;
-        L = eng.legal(M, O);
         uint32_t rl = 0;
         if (rng.init_rand > 0)
             rl = (uint32_t)scale_index(philox_x(rng.seed, id, g, RNG_OPENING_AUTO), rng.init_rand / 2 + 1) * 2u;
