@@ -640,6 +640,41 @@ def observe_lines(n, sizes, dev, stream, launches=50):
     return out
 
 
+def config1_line(dev, seconds=0.5):
+    """BASELINE config 1: ONE 8x8 board through the drop-in OthelloEnv
+    (othello.py:96-214), random protagonist against RandomPolicy, reset after
+    each game, for a bounded wall time.  Every step synchronises (the drop-in
+    returns host values, as the reference does), so this is the per-call latency
+    of the device path, not throughput; the reference's own Python runs
+    6.6-8.5 x 10^3 plies/s per core."""
+    import contextlib
+    import io
+
+    import numpy as np
+
+    from gymothelloenv_amd import OthelloEnv
+    from gymothelloenv_amd.policies import RandomPolicy
+    rnd = np.random.RandomState(0)
+    env = OthelloEnv(white_policy=RandomPolicy(1), black_policy=RandomPolicy(1), protagonist=1, device=dev)
+    calls = games = 0
+    with contextlib.redirect_stdout(io.StringIO()):  # reset() prints, as the reference's does
+        env.reset()
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            moves = env.possible_moves
+            _, _, done, _ = env.step(moves[rnd.randint(0, len(moves))])
+            calls += 1
+            if done:
+                games += 1
+                env.reset()
+        dt = time.perf_counter() - t0
+    env.close()
+    return {"workload": "config1: one 8x8 board, OthelloEnv drop-in, random vs RandomPolicy",
+            "env_steps_per_s": calls / dt, "us_per_step": dt / calls * 1e6, "steps": calls, "games": games,
+            "note": "each step() synchronises and returns host values (the reference's API); latency, not "
+                    "throughput"}
+
+
 def side_measurements(env, policy, E, n, W, dev, stream):
     """Beside the headline (never `value`): the per-step paths with the state
     through HBM every ply -- oth_step with external actions (`step_external`)
@@ -658,6 +693,7 @@ def side_measurements(env, policy, E, n, W, dev, stream):
                       "config5_random": [play_line("random", nb, CONFIG2_BOARDS, 100, 0, dev, stream)
                                          for nb in (6, 10)]}
     out["observe"] = observe_lines(n, (E, 1048576), dev, stream)
+    out["configs"]["config1_single_board"] = config1_line(dev)
     big = VecOthelloEnv(1048576, board_size=n, auto_reset=True, seed=0, device=dev)
     big.step_policy(policy, n_plies=20, record=False)
     out["single_ply_launches"] = [single_ply(env, policy, E, W, dev, stream),

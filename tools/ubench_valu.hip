@@ -72,6 +72,39 @@ __global__ void half_shl64(uint64_t* out, int iters) {
     out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
 }
 
+// multi-pass candidates (round 4): 32-bit multiplies (byte broadcasts of RayMath,
+// scale_index), the 32x32->64 multiply-add of Philox, and the full-rate ops that
+// could stand in for them (v_perm_b32 byte broadcast, v_mul_u32_u24)
+#define IND8X(op)                                                                                       \
+    asm volatile(op " %0, %0, %1" : "+v"(a0) : "v"(m)); asm volatile(op " %0, %0, %1" : "+v"(a1) : "v"(m)); \
+    asm volatile(op " %0, %0, %1" : "+v"(a2) : "v"(m)); asm volatile(op " %0, %0, %1" : "+v"(a3) : "v"(m)); \
+    asm volatile(op " %0, %0, %1" : "+v"(a4) : "v"(m)); asm volatile(op " %0, %0, %1" : "+v"(a5) : "v"(m)); \
+    asm volatile(op " %0, %0, %1" : "+v"(a6) : "v"(m)); asm volatile(op " %0, %0, %1" : "+v"(a7) : "v"(m));
+#define IND_KERNEL2(name, op)                                                                    \
+    __global__ void name(uint64_t* out, int iters) {                                             \
+        uint32_t a0 = 1, a1 = 2, a2 = 3, a3 = 4, a4 = 5, a5 = 6, a6 = 7, a7 = threadIdx.x, m = 3; \
+        for (int i = 0; i < iters; ++i) { REP8(IND8X(op)) }                                      \
+        out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;      \
+    }
+IND_KERNEL2(ind_mullo, "v_mul_lo_u32")
+IND_KERNEL2(ind_mulhi, "v_mul_hi_u32")
+IND_KERNEL2(ind_mul24, "v_mul_u32_u24")
+IND_KERNEL2(ind_bcnt, "v_bcnt_u32_b32")
+__global__ void ind_perm(uint64_t* out, int iters) {
+    uint32_t a0 = 1, a1 = 2, a2 = 3, a3 = 4, a4 = 5, a5 = 6, a6 = 7, a7 = threadIdx.x, m = 0x04040404u, c = 0;
+    for (int i = 0; i < iters; ++i) { REP8(IND8O("v_perm_b32")) }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+#define MAD1(o, a) asm volatile("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(o), "=s"(sc) : "v"(a), "v"(m));
+__global__ void ind_mad64(uint64_t* out, int iters) {
+    uint32_t a0 = 1, a1 = 2, a2 = 3, a3 = 4, a4 = 5, a5 = 6, a6 = 7, a7 = threadIdx.x, m = 0xD2511F53u;
+    uint64_t o0 = 0, o1 = 0, o2 = 0, o3 = 0, o4 = 0, o5 = 0, o6 = 0, o7 = 0, sc;
+    for (int i = 0; i < iters; ++i) {
+        REP8(MAD1(o0, a0) MAD1(o1, a1) MAD1(o2, a2) MAD1(o3, a3) MAD1(o4, a4) MAD1(o5, a5) MAD1(o6, a6) MAD1(o7, a7))
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = o0 ^ o1 ^ o2 ^ o3 ^ o4 ^ o5 ^ o6 ^ o7;
+}
+
 typedef void (*K)(uint64_t*, int);
 
 static float run(K k, int waves_per_simd, int iters, uint64_t* buf) {
@@ -97,11 +130,13 @@ int main() {
         {"dep v_lshlrev_b64", dep_shl64, 64}, {"dep v_and_b32", dep_and32, 64},
         {"ind v_lshlrev_b64", ind_shl64, 64}, {"ind v_and_b32", ind_and32, 64},
         {"ind v_and_or_b32", ind_andor32, 64}, {"half-wave ind v_and_b32", half_and32, 64},
-        {"half-wave dep v_and_b32", half_dep_and32, 64}, {"half-wave ind v_lshlrev_b64", half_shl64, 64}};
+        {"half-wave dep v_and_b32", half_dep_and32, 64}, {"half-wave ind v_lshlrev_b64", half_shl64, 64},
+        {"ind v_mul_lo_u32", ind_mullo, 64}, {"ind v_mul_hi_u32", ind_mulhi, 64}, {"ind v_mul_u32_u24", ind_mul24, 64},
+        {"ind v_bcnt_u32_b32", ind_bcnt, 64}, {"ind v_perm_b32", ind_perm, 64}, {"ind v_mad_u64_u32", ind_mad64, 64}};
     printf("{\"clock_note\": \"cycles assume 2.4 GHz\", \"results\": [\n");
     bool first = true;
     for (auto& t : ks)
-        for (int w : {1, 2, 4, 8}) {
+        for (int w : {1, 2, 4}) {
             float ms = run(t.k, w, iters, buf);
             double ns_per_op = ms * 1e6 / ((double)iters * t.ops_per_iter);  // per wave-op on one SIMD (w waves share it)
             printf("%s{\"op\": \"%s\", \"waves_per_simd\": %d, \"ns_per_wave_op_per_simd\": %.4f, \"cycles_per_wave_op\": %.3f}",
