@@ -1810,7 +1810,14 @@ __global__ __launch_bounds__(BLOCK) void k_observe_w(const uint64_t* __restrict_
         return r;
     };
     // every lane takes part in every step (ds_bpermute reads an inactive source lane
-    // as 0): the last step's lanes past the region clamp their quad and skip the store
+    // as 0): the last step's lanes past the region clamp their quad and skip the store.
+    // Measured and not kept (1,048,576 boards, make_state f32; a plain torch fill of the
+    // same tensor: 155 us, ours 219): the waves starting their regions at different
+    // steps 217.8 -> 225.8 us; boards dealt to the waves with the grid's stride (the
+    // resident waves store into one window) 219.6 -> 264.3; the step's board words by
+    // v_readlane 218.9 -> 217.5; the loop unrolled by 4 +-0; 128 / 256 boards per wave
+    // (every wave resident at once, all loads first) 218.8 -> 216.6 / 234.4, and at
+    // 262,144 boards 46.5 -> 57.6 / 110.3 (profiles/r04/obs/)
     for (int g0 = 0; g0 < total; g0 += 64) {
         const int g = g0 + lane < total ? g0 + lane : total - 1;
         const int kb = g / PQ, rr = g - kb * PQ;
