@@ -1815,36 +1815,51 @@ __global__ __launch_bounds__(BLOCK) void k_observe_w(const uint64_t* __restrict_
     // same tensor: 155 us, ours 219): the waves starting their regions at different
     // steps 217.8 -> 225.8 us; boards dealt to the waves with the grid's stride (the
     // resident waves store into one window) 219.6 -> 264.3; the step's board words by
-    // v_readlane 218.9 -> 217.5; the loop unrolled by 4 +-0; 128 / 256 boards per wave
-    // (every wave resident at once, all loads first) 218.8 -> 216.6 / 234.4, and at
-    // 262,144 boards 46.5 -> 57.6 / 110.3 (profiles/r04/obs/)
+    // v_readlane 218.9 -> 217.5 (and +-0 again on the branch-free body below); the loop
+    // unrolled by 4 +-0; 128 / 256 boards per wave (every wave resident at once, all
+    // loads first) 218.8 -> 216.6 / 234.4, and at 262,144 boards 46.5 -> 57.6 / 110.3
+    // (profiles/r04/obs/)
     for (int g0 = 0; g0 < total; g0 += 64) {
-        const int g = g0 + lane < total ? g0 + lane : total - 1;
-        const int kb = g / PQ, rr = g - kb * PQ;
-        const int plane = rr / Q, q = rr - plane * Q;
-        const int a0 = 4 * q, wi = a0 / 64, bi = a0 % 64;  // 4 | 64: a quad never straddles words
-        const uint32_t nbk = (uint32_t)(fetch(bw, kb, wi) >> bi) & 0xFu;
-        const uint32_t nwk = (uint32_t)(fetch(ww, kb, wi) >> bi) & 0xFu;
-        const uint32_t flk = (uint32_t)__shfl((int)fl, kb);
+        const uint32_t g = (uint32_t)(g0 + lane < total ? g0 + lane : total - 1);
+        const uint32_t kb = g / PQ, rr = g - kb * PQ;
+        const uint32_t plane = rr / Q, q = rr - plane * Q;
+        const uint32_t a0 = 4 * q, wi = a0 / 64, bi = a0 % 64;  // 4 | 64: a quad never straddles words
+        const uint64_t xb = fetch(bw, (int)kb, (int)wi), xw = fetch(ww, (int)kb, (int)wi);
+        const uint32_t flk = (uint32_t)__shfl((int)fl, (int)kb);
         const bool tw = (flk & 1u) != 0;
-        uint32_t nl = 0;
-        if constexpr (NEED_L) nl = (uint32_t)(fetch(lw, kb, wi) >> bi) & 0xFu;
+        uint64_t xl = 0;
+        if constexpr (NEED_L) xl = fetch(lw, (int)kb, (int)wi);
+        // the lanes of one store cover several planes: each lane's plane word is
+        // picked by masks, not branches (the compiler had made the plane choice
+        // branches, so the wave ran every plane's path in turn with exec-mask SALU
+        // between them): make_state f32 at 65,536 / 262,144 / 1,048,576 boards
+        // 13.75 -> 12.79 / 46.6 -> 41.5 / 219.8 -> 208.3 us, int64 board 1,048,576
+        // 104.7 -> 102.4 (profiles/r04/obs/ab_branchfree.jsonl)
         int v[4];
         if constexpr (LAYOUT == OTH_OBS_LEGAL) {  // possible_moves
+            const uint32_t nl = (uint32_t)(xl >> bi) & 0xFu;
 #pragma unroll
             for (int j = 0; j < 4; ++j) v[j] = (int)((nl >> j) & 1u);
         } else if constexpr (LAYOUT == OTH_OBS_ABSOLUTE) {  // othello.py:257
+            const uint32_t nbk = (uint32_t)(xb >> bi) & 0xFu, nwk = (uint32_t)(xw >> bi) & 0xFu;
 #pragma unroll
             for (int j = 0; j < 4; ++j) v[j] = (int)((nwk >> j) & 1u) - (int)((nbk >> j) & 1u);
         } else if constexpr (LAYOUT == OTH_OBS_MAKE_STATE) {  // util.py:48-74
-            uint32_t bits = plane == 0 ? nbk : (plane == 1 ? nwk : (plane == 2 ? (tw ? 0xFu : 0u) : ((flk & 2u) ? nl : 0u)));
+            const uint64_t m0 = 0ull - (uint64_t)(plane == 0u), m1 = 0ull - (uint64_t)(plane == 1u);
+            const uint64_t m2 = 0ull - (uint64_t)(plane == 2u && tw), m3 = 0ull - (uint64_t)(plane == 3u && (flk & 2u));
+            const uint32_t bits = (uint32_t)(((xb & m0) | (xw & m1) | (xl & m3) | m2) >> bi) & 0xFu;
 #pragma unroll
             for (int j = 0; j < 4; ++j) v[j] = (int)((bits >> j) & 1u);
         } else {  // othello.py:363-376: mover +1, opponent -1; plane 1 the legal squares
-            const uint32_t mv = tw ? nwk : nbk, op = tw ? nbk : nwk;
+            const uint64_t xm = tw ? xw : xb, xo = tw ? xb : xw;
+            const uint32_t mv = (uint32_t)(xm >> bi) & 0xFu, op = (uint32_t)(xo >> bi) & 0xFu;
+            const uint32_t nl = (uint32_t)(xl >> bi) & 0xFu;
+            const bool p1 = plane != 0u;
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                v[j] = plane == 0 ? (int)((mv >> j) & 1u) - (int)((op >> j) & 1u) : (int)((nl >> j) & 1u);
+            for (int j = 0; j < 4; ++j) {
+                const int b = (int)((mv >> j) & 1u) - (int)((op >> j) & 1u);
+                v[j] = p1 ? (int)((nl >> j) & 1u) : b;
+            }
         }
         if (g0 + lane < total) put_quad<T>(base, (uint32_t)g, v[0], v[1], v[2], v[3]);
     }
