@@ -532,6 +532,46 @@ def step_external(E, n, dev, stream, plies=64):
             "replay_equals_recording": same}
 
 
+def vs_line(E, n, dev, stream, calls=64, opponent="random"):
+    """OthelloEnv's turn loop on the device (othello.py:151-200; oth_reset_vs /
+    oth_step_vs): a greedy protagonist (oth_policy_actions, GreedyPolicy
+    simple_policies.py:69-92) against the embedded `opponent` on E boards with
+    auto-reset and 0-10-ply random openings (without them every greedy-vs-greedy
+    game is the same), the README's evaluation protocol batched.  One call = the
+    protagonist's greedy move + its step + the opponent's replies until the
+    protagonist is to move again; `calls` calls captured in a HIP graph (median of 5
+    replays).  env-steps counted = plies applied (the `plies` output: one
+    protagonist ply plus the opponent's)."""
+    import torch
+
+    from gymothelloenv_amd import VecOthelloEnv
+    env = VecOthelloEnv(E, board_size=n, auto_reset=True, seed=11, device=dev, initial_rand_steps=10)
+    env.reset_vs(opponent, protagonist=1)
+    plies = torch.zeros(calls, E, dtype=torch.int32, device=dev)
+
+    def call(i):
+        _, _, _, p = env.step_vs(env.policy_actions("greedy"), opponent, observe=False)
+        plies[i].copy_(p)
+    for i in range(4):
+        call(i)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g), env.graph_region():
+        for i in range(calls):
+            call(i)
+    reps = []
+    for _ in range(5):
+        reps.append(_time_launches(stream, lambda i: g.replay(), 1) / calls)
+    us = statistics.median(reps)
+    applied = int(plies.sum().item())  # plies of the last replay
+    wdl = [int(x) for x in env.counts_vs()]
+    env.close()
+    return {"workload": "othello-env-vs-%s-8x8-E%d" % (opponent, E), "boards": E,
+            "kernels": "k_policy_actions<greedy> + k_step_vs<%s>" % opponent, "us_per_call": us,
+            "plies_per_call": applied / calls, "env_steps_per_s": applied / calls / (us * 1e-6),
+            "protagonist_wdl": wdl, "timing": "HIP graph of %d calls, median of 5 replays" % calls}
+
+
 def single_ply(env, policy, E, W, dev, stream, k=64):
     """oth_step_policy with one ply per launch (k_ply_rand for random play on
     one-word boards): every board's state through HBM every ply.  k launches
@@ -694,6 +734,7 @@ def side_measurements(env, policy, E, n, W, dev, stream):
                                          for nb in (6, 10)]}
     out["observe"] = observe_lines(n, (E, 1048576), dev, stream)
     out["configs"]["config1_single_board"] = config1_line(dev)
+    out["othello_env_vs"] = [vs_line(E, n, dev, stream, opponent=o) for o in ("random", "greedy")]
     big = VecOthelloEnv(1048576, board_size=n, auto_reset=True, seed=0, device=dev)
     big.step_policy(policy, n_plies=20, record=False)
     out["single_ply_launches"] = [single_ply(env, policy, E, W, dev, stream),
