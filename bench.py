@@ -547,27 +547,27 @@ def vs_line(E, n, dev, stream, calls=64, opponent="random"):
     from gymothelloenv_amd import VecOthelloEnv
     env = VecOthelloEnv(E, board_size=n, auto_reset=True, seed=11, device=dev, initial_rand_steps=10)
     env.reset_vs(opponent, protagonist=1)
-    plies = torch.zeros(calls, E, dtype=torch.int32, device=dev)
+    plies = []  # each call's plies-applied tensor (graph memory: holds the last replay's values)
 
-    def call(i):
-        _, _, _, p = env.step_vs(env.policy_actions("greedy"), opponent, observe=False)
-        plies[i].copy_(p)
-    for i in range(4):
-        call(i)
+    def call():
+        return env.step_vs(env.policy_actions("greedy"), opponent, observe=False)[3]
+    for _ in range(4):
+        call()
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g), env.graph_region():
-        for i in range(calls):
-            call(i)
+        for _ in range(calls):
+            plies.append(call())
     reps = []
     for _ in range(5):
         reps.append(_time_launches(stream, lambda i: g.replay(), 1) / calls)
     us = statistics.median(reps)
-    applied = int(plies.sum().item())  # plies of the last replay
+    applied = int(sum(int(p.sum().item()) for p in plies))  # plies of the last replay
     wdl = [int(x) for x in env.counts_vs()]
     env.close()
     return {"workload": "othello-env-vs-%s-8x8-E%d" % (opponent, E), "boards": E,
-            "kernels": "k_policy_actions<greedy> + k_step_vs<%s>" % opponent, "us_per_call": us,
+            "kernels": "k_policy_actions<greedy> + k_step_vs%s<%s>" % ("1" if n <= 8 else "", opponent),
+            "us_per_call": us,
             "plies_per_call": applied / calls, "env_steps_per_s": applied / calls / (us * 1e-6),
             "protagonist_wdl": wdl, "timing": "HIP graph of %d calls, median of 5 replays" % calls}
 

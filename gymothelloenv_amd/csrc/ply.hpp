@@ -210,10 +210,12 @@ __device__ __forceinline__ uint64_t scan1(uint64_t P, uint64_t O, const PairAxes
 // [0, N*N) then).  Returns reward / done / winner (0 unless the game ended).
 // RAYS_PAIR: lane h of a pair holding the same board (the flips and the
 // legal scans split over the pair; every result is the same on both lanes).
-template <int N, int RAYS = RAYS_MATH>
+// KEEP (one lane per board): the next mover's eight fills (OneWord::legal's t)
+// into tk, for a greedy pick that follows without a scan of its own.
+template <int N, int RAYS = RAYS_MATH, bool KEEP = false>
 __device__ __forceinline__ void step1(uint64_t& B, uint64_t& Wt, uint64_t& L, uint32_t& m, int a, bool valid,
                                       uint32_t flags, const uint64_t* __restrict__ rays, int& reward, int& done,
-                                      int& winner, int h = 0) {
+                                      int& winner, int h = 0, uint64_t* tk = nullptr) {
     constexpr uint64_t BD = Geo<N>::BOARD.w[0];
     constexpr int NN = N * N;
     const bool tw = (m & M_TURN_WHITE) != 0;
@@ -226,9 +228,14 @@ __device__ __forceinline__ void step1(uint64_t& B, uint64_t& Wt, uint64_t& L, ui
     const bool sudden = !valid && (flags & OTH_SUDDEN_DEATH);              // :427
     const bool stale = sudden || full;  // :431-433: turn and possible_moves stay as they were
     const PairAxes ax = pair_axes<N>(h);
-    uint64_t nl = scan1<N, RAYS>(O, P, ax);                                 // :436
+    uint64_t nl;
+    if constexpr (KEEP) nl = OneWord<N>::legal(O, P, tk);                  // :436
+    else nl = scan1<N, RAYS>(O, P, ax);
     const bool opp_pass = nl == 0;
-    if (opp_pass && !stale) nl = scan1<N, RAYS>(P, O, ax);                  // :437-440
+    if (opp_pass && !stale) {                                               // :437-440
+        if constexpr (KEEP) nl = OneWord<N>::legal(P, O, tk);
+        else nl = scan1<N, RAYS>(P, O, ax);
+    }
     const bool term = stale || (opp_pass && nl == 0);                       // :441-442
     const int pc = popc64(P), oc = popc64(O);
     const int cur = tw ? WHITE_DISK : BLACK_DISK;
@@ -380,6 +387,139 @@ __global__ __launch_bounds__(BLOCK) void k_ply_rand(uint64_t* __restrict__ board
                                                     uint8_t* __restrict__ dones, unsigned long long* __restrict__ wdl,
                                                     const uint64_t* __restrict__ rays, Rng rng, uint64_t ply) {
     ply_body<N, PLY_RANDOM, RAYS>(boards, meta, legal, E, flags, actions, rewards, dones, wdl, rays, rng, ply);
+}
+
+// OthelloEnv.step (othello.py:176-200) on one-word boards against a random or
+// greedy opponent: k_step_vs's control flow (device.hpp: the opponent's replies
+// before and after the protagonist's ply, random-opening plies, the reward
+// negated after opponent plies, the W/D/L tallies, the auto-reset with the
+// opponent's opening reply) with every ply through step1 (computed rays,
+// branch-free but for the pass re-scan) on the board held as four registers
+// instead of the generic Lane / Solo engine.  Results are identical.
+template <int N, int POLICY>
+__global__ __launch_bounds__(BLOCK) void k_step_vs1(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
+                                                    uint64_t* __restrict__ legal, int E, uint32_t flags,
+                                                    const int32_t* __restrict__ actions,
+                                                    const int8_t* __restrict__ prot, int32_t* __restrict__ rewards,
+                                                    uint8_t* __restrict__ dones, int32_t* __restrict__ plies_out,
+                                                    unsigned long long* __restrict__ wdl,
+                                                    unsigned long long* __restrict__ wdl_vs, Rng rng, uint64_t call) {
+    static_assert(Geo<N>::W == 1, "one-word boards");
+    static_assert(POLICY == OTH_POLICY_RANDOM || POLICY == OTH_POLICY_GREEDY, "random or greedy opponent");
+    constexpr int NN = N * N;
+    __shared__ uint64_t no_table[1];  // step1's ray table argument (RAYS_MATH reads none)
+    call += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    // per-wave W/D/L slots (ballots, no LDS, no barrier: the waves of a block end
+    // after different numbers of opponent plies), read with the first loads
+    WaveSlot slot(wdl, e, E), slot_vs(wdl_vs, e, E);
+    uint32_t cb = 0, cd = 0, cw = 0, pw_n = 0, pd_n = 0, pl_n = 0;
+    if (e < E) {
+        const uint32_t id = rng.id_base + (uint32_t)e;
+        const bool pw = prot ? prot[e] == WHITE_DISK : true;
+        const uint64_t gbase = call * VS_PLIES_PER_CALL;
+        const ulonglong2 bw = reinterpret_cast<const ulonglong2*>(boards)[e];
+        uint64_t B = bw.x, Wt = bw.y, L = legal[e];
+        uint32_t m = meta[e];
+        int act = actions[e];
+        uint32_t j = 0;
+        int r = 0, d = 1, win = NO_DISK, plies = 0;
+        // greedy: the side to move's fills, carried from the scan of the ply before
+        // (step1<KEEP>) so that a greedy pick needs no scan of its own
+        constexpr bool KEEP = POLICY == OTH_POLICY_GREEDY;
+        uint64_t t[8];
+        bool have_t = false;
+        // one ply of the side to move: a (any square; the invalid path when it is not
+        // in possible_moves, as step_lane)
+        auto ply = [&](int a) __attribute__((always_inline)) {
+            const bool valid = (unsigned)a < (unsigned)NN && ((L >> (a & 63)) & 1ull);
+            step1<N, RAYS_MATH, KEEP>(B, Wt, L, m, a, valid, flags, no_table, r, d, win, 0, t);
+            have_t = true;
+        };
+        auto random_pick = [&](uint64_t g) __attribute__((always_inline)) {  // random_action: -1 without a move
+            const int n = popc64(L);
+            return n ? select64(L, scale_index(action_draw(rng.seed, id, g), n)) : -1;
+        };
+        // opponent_reply: the opponent moves while it is to move and the game is on
+        auto reply = [&](bool openings) __attribute__((always_inline)) {
+            while (!(m & M_TERMINATED) && (((m & M_TURN_WHITE) != 0) != pw)) {
+                const uint32_t rl = m >> M_RAND_SHIFT;
+                const uint64_t g = gbase + j++;
+                int a;
+                if (POLICY == OTH_POLICY_RANDOM || (openings && rl > 0)) {
+                    a = random_pick(g);
+                } else {  // GreedyPolicy from the mover's fills (greedy_action)
+                    if (!have_t) {
+                        const bool tw = (m & M_TURN_WHITE) != 0;
+                        (void)OneWord<N>::legal(tw ? Wt : B, tw ? B : Wt, t);
+                        have_t = true;
+                    }
+                    a = OneWord<N>::greedy(t, L);
+                }
+                if (openings && rl > 0) m -= 1u << M_RAND_SHIFT;
+                ply(a);
+            }
+        };
+        if (!(m & M_TERMINATED)) {
+            d = 0;
+            reply(true);  // the protagonist must be to move (othello.py:177): else the opponent replies first
+            if (!(m & M_TERMINATED)) {
+                const uint32_t rl = m >> M_RAND_SHIFT;
+                const uint64_t g = gbase + j++;
+                if (rl > 0) {  // opening ply: the protagonist's action is replaced too (:179-182)
+                    act = random_pick(g);
+                    m -= 1u << M_RAND_SHIFT;
+                }
+                ply(act);
+                if (!d) {
+                    reply(true);
+                    r = -r;  // :200
+                }
+            } else {
+                r = -r;
+            }
+            plies = (int)j;
+            if (d) {
+                cb = win == BLACK_DISK;
+                cd = win == NO_DISK;
+                cw = win == WHITE_DISK;
+                const int pcol = pw ? WHITE_DISK : BLACK_DISK;  // run.py:100-130's count
+                pw_n = win == pcol;
+                pd_n = win == NO_DISK;
+                pl_n = win == -pcol;
+                if (flags & OTH_AUTO_RESET) {  // reset_vs_lane: reset, then the opponent's opening reply
+                    B = Start<N>::BLACK.w[0];
+                    Wt = Start<N>::WHITE.w[0];
+                    constexpr uint64_t START_MOVES = start_moves<N>();
+                    L = START_MOVES;
+                    uint32_t rl = 0;
+                    if (rng.init_rand > 0)
+                        rl = (uint32_t)scale_index(philox_x(rng.seed, id, call, RNG_OPENING_AUTO),
+                                                   rng.init_rand / 2 + 1) * 2u;
+                    m = (rl & 0xffu) << M_RAND_SHIFT;
+                    if constexpr (KEEP) {  // the start position's fills (black to move)
+                        constexpr StartFills<N> SF = start_fills<N>();
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) t[k] = SF.t[k];
+                        have_t = true;
+                    }
+                    const int rs = r, ds = d, ws = win;  // (the reply's reward / done are not
+                    reply(false);                         // reported, as in reset_vs_lane)
+                    r = rs, d = ds, win = ws;
+                }
+            }
+        }
+        reinterpret_cast<ulonglong2*>(boards)[e] = ulonglong2{B, Wt};
+        legal[e] = L;
+        meta[e] = (uint16_t)m;
+        if (rewards) rewards[e] = r;
+        if (dones) dones[e] = (uint8_t)d;
+        if (plies_out) plies_out[e] = plies;
+    }
+    slot.count(cb != 0, cd != 0, cw != 0);
+    slot.flush();
+    slot_vs.count(pw_n != 0, pd_n != 0, pl_n != 0);
+    slot_vs.flush();
 }
 
 // oth_create: the handle's tables in device memory: the ray table (fill_rays<N,
