@@ -456,6 +456,44 @@ def test_vs_rollout_replays_on_oracle(torch_cuda, n, opp, init_rand):
     np.testing.assert_array_equal(env.counts().cpu().numpy(), wdl)
 
 
+@pytest.mark.parametrize("n,opp,sd,dr,auto", [(8, "random", False, True, True), (8, "greedy", False, False, False),
+                                              (8, "random", True, True, False), (6, "greedy", False, True, True),
+                                              (10, "greedy", False, True, True)])
+def test_vs_flag_combinations_on_oracle(torch_cuda, n, opp, sd, dr, auto):
+    """OthelloEnv.step on the device (k_step_vs1 on one-word boards, k_step_vs on
+    10x10) with the other env flags: invalid protagonist actions without sudden
+    death (the turn passes, othello.py:417-427), disk-count rewards (:446-459)
+    negated after opponent plies (:200), and boards left terminated without
+    auto-reset (a step on them reports done); rewards / dones / plies / state /
+    protagonist W/D/L equal the oracle's every call."""
+    torch = torch_cuda
+    E, calls = 2048, 60
+    pol = 0 if opp == "random" else 1
+    prot = np.where(np.arange(E) % 3 == 0, -1, 1).astype(np.int8)
+    env = make_env(torch, E, n, sd=sd, dr=dr, auto=auto, seed=19, init_rand=4)
+    env.reset_vs(opp, protagonist=torch.from_numpy(prot))
+    flags = flags_of(sd, dr, auto)
+    s = oracle.reset_vs(n, E, flags, pol, 0, seed=19, initial_rand_steps=4, prot=prot)
+    rng = np.random.RandomState(100 + n)
+    wdl = np.zeros(3, dtype=np.int64)
+    for c in range(1, calls + 1):
+        lb = legal_bool(s.legal, n)
+        pick = np.argmax(rng.rand(E, n * n) * lb, axis=1).astype(np.int32)
+        acts = np.where((rng.rand(E) < 0.05) | ~lb.any(axis=1), rng.randint(-1, n * n, size=E), pick).astype(np.int32)
+        orw, od, opl = oracle.step_vs(s, flags, pol, c, acts, seed=19, initial_rand_steps=4, prot=prot, wdl=wdl)
+        _, rew, dn, plies = env.step_vs(torch.from_numpy(acts).cuda(), opp, observe=False)
+        np.testing.assert_array_equal(rew.cpu().numpy(), orw)
+        np.testing.assert_array_equal(dn.cpu().numpy(), od.astype(bool))
+        np.testing.assert_array_equal(plies.cpu().numpy(), opl)
+    b, m, lg = get_state_np(env)
+    np.testing.assert_array_equal(b, s.boards)
+    np.testing.assert_array_equal(m, s.meta)
+    np.testing.assert_array_equal(lg, s.legal)
+    np.testing.assert_array_equal(env.counts().cpu().numpy(), wdl)
+    if not auto:
+        assert (m & 2).any(), "no board finished: the no-auto-reset path is untested"
+
+
 @pytest.mark.parametrize("n,depth", [(6, 1), (6, 2), (6, 3), (8, 1), (8, 2), (8, 3), (6, 4), (6, 5), (8, 4),
                                      (4, 6), (4, 7), (4, 8), (4, 9), (4, 10), (5, 6), (5, 7), (6, 6), (8, 6)])
 def test_maximin_actions_match_reference(torch_cuda, golden_dir, n, depth):
