@@ -1816,7 +1816,7 @@ __global__ __launch_bounds__(BLOCK) void k_observe_w(const uint64_t* __restrict_
     // steps 217.8 -> 225.8 us; boards dealt to the waves with the grid's stride (the
     // resident waves store into one window) 219.6 -> 264.3; the step's board words by
     // v_readlane 218.9 -> 217.5 (and +-0 again on the branch-free body below); the loop
-    // unrolled by 4 +-0; 128 / 256 boards per wave (every wave resident at once, all
+    // unrolled by 4 +-0 (by 2 / 4 on the branch-free body: +-0, profiles/r04/obs/ab_unroll_bf.jsonl); 128 / 256 boards per wave (every wave resident at once, all
     // loads first) 218.8 -> 216.6 / 234.4, and at 262,144 boards 46.5 -> 57.6 / 110.3
     // (profiles/r04/obs/)
     for (int g0 = 0; g0 < total; g0 += 64) {
