@@ -33,8 +33,19 @@ int hip_fail(hipError_t err, const char* where) {
     return OTH_EHIP;
 }
 
+namespace {
+thread_local hipError_t g_launch_err = hipSuccess;  // the first failed launch since after_launch
+}
+
+void note_launch(hipError_t err) {
+    if (err != hipSuccess && g_launch_err == hipSuccess) g_launch_err = err;
+}
+
 int after_launch(const char* what) {
-    hipError_t err = hipGetLastError();
+    hipError_t err = g_launch_err;
+    g_launch_err = hipSuccess;
+    const hipError_t last = hipGetLastError();  // (and clears HIP's own sticky status)
+    if (err == hipSuccess) err = last;
     if (err != hipSuccess) return hip_fail(err, what);
     return OTH_OK;
 }
@@ -360,8 +371,8 @@ int oth_graph_end(oth_env* env, uint64_t d_sample, int32_t enqueue, uint64_t* d_
     if (d_ply) *d_ply = dp;
     if (!enqueue) return OTH_OK;
     OTH_CHECK_ENV(env);
-    hipLaunchKernelGGL(k_graph_advance, dim3(1), dim3(64), 0, (hipStream_t)stream, env->ctr_slots + 2 * k, dp,
-                       d_sample);
+    launch_k(k_graph_advance, dim3(1), dim3(64), 0, (hipStream_t)stream, env->ctr_slots + 2 * k, dp,
+             d_sample);
     return oth_host::after_launch("oth_graph_end");
 }
 
@@ -434,15 +445,15 @@ int oth_counts(oth_env* env, int64_t* out, int32_t reset, oth_stream_t stream) {
     OTH_CHECK_ENV(env);
     if (!out) return fail(OTH_EINVAL, "out is NULL");
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_reduce_wdl, dim3(1), dim3(256), 0, s, env->wdl, env->nslots, out, reset ? 1 : 0);
+    launch_k(k_reduce_wdl, dim3(1), dim3(256), 0, s, env->wdl, env->nslots, out, reset ? 1 : 0);
     return after_launch("oth_counts");
 }
 
 int oth_counts_vs(oth_env* env, int64_t* out, int32_t reset, oth_stream_t stream) {
     OTH_CHECK_ENV(env);
     if (!out) return fail(OTH_EINVAL, "out is NULL");
-    hipLaunchKernelGGL(k_reduce_wdl, dim3(1), dim3(256), 0, (hipStream_t)stream, env->wdl_vs, env->nslots, out,
-                       reset ? 1 : 0);
+    launch_k(k_reduce_wdl, dim3(1), dim3(256), 0, (hipStream_t)stream, env->wdl_vs, env->nslots, out,
+             reset ? 1 : 0);
     return after_launch("oth_counts_vs");
 }
 

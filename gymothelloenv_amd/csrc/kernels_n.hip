@@ -46,8 +46,8 @@ int with_policy(int policy, Fn&& fn) {
 
 template <int N>
 int launch_reset(oth_env* env, const uint8_t* mask, hipStream_t st) {
-    hipLaunchKernelGGL(k_reset<N>, dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards, env->meta, env->legal,
-                       env->E, mask, rng_of(env), env->ply);
+    launch_k(k_reset<N>, dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards, env->meta, env->legal,
+             env->E, mask, rng_of(env), env->ply);
     return after_launch("oth_reset");
 }
 
@@ -55,7 +55,7 @@ int launch_reset(oth_env* env, const uint8_t* mask, hipStream_t st) {
 template <int N>
 int launch_fill_rays(oth_env* env, hipStream_t st) {
     if constexpr (Geo<N>::W == 1) {
-        hipLaunchKernelGGL(k_fill_rays<N>, dim3(1), dim3(BLOCK), 0, st, env->rays);
+        launch_k(k_fill_rays<N>, dim3(1), dim3(BLOCK), 0, st, env->rays);
         return after_launch("oth_create: ray table");
     }
     return OTH_OK;
@@ -66,17 +66,17 @@ int launch_step(oth_env* env, const int32_t* actions, int32_t* rewards, uint8_t*
                 hipStream_t st) {
     if constexpr (Geo<N>::W == 1) {  // the single-ply kernel (ply.hpp)
         if (env->E <= OTH_PLY_MATH_MAX_E)
-            hipLaunchKernelGGL((k_ply_step<N, RAYS_MATH>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards,
-                               env->meta, env->legal, env->E, env->flags, actions, rewards, dones, env->wdl, env->rays,
-                               rng_of(env), ply);
+            launch_k((k_ply_step<N, RAYS_MATH>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards,
+                     env->meta, env->legal, env->E, env->flags, actions, rewards, dones, env->wdl, env->rays,
+                     rng_of(env), ply);
         else
-            hipLaunchKernelGGL((k_ply_step<N, RAYS_HALF>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st,
-                               env->boards, env->meta, env->legal, env->E, env->flags, actions, rewards, dones,
-                               env->wdl, env->rays, rng_of(env), ply);
+            launch_k((k_ply_step<N, RAYS_HALF>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st,
+                     env->boards, env->meta, env->legal, env->E, env->flags, actions, rewards, dones,
+                     env->wdl, env->rays, rng_of(env), ply);
         return after_launch("oth_step");
     }
-    hipLaunchKernelGGL(k_step<N>, dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards, env->meta, env->legal,
-                       env->E, env->flags, actions, rewards, dones, env->wdl, rng_of(env), ply);
+    launch_k(k_step<N>, dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards, env->meta, env->legal,
+             env->E, env->flags, actions, rewards, dones, env->wdl, rng_of(env), ply);
     return after_launch("oth_step");
 }
 
@@ -89,13 +89,13 @@ void launch_k_play(int lanes_per_board, oth_env* env, int policy, int n_plies, i
     if constexpr (POL == OTH_POLICY_RANDOM && Geo<N>::W == 1) {
         if (n_plies == 1) {  // one ply per launch: the single-ply kernel (ply.hpp), any flags
             if (env->E <= OTH_PLY_MATH_MAX_E)
-                hipLaunchKernelGGL((k_ply_rand<N, RAYS_MATH>), dim3(grid_for(env->E)), block, 0, st, env->boards,
-                                   env->meta, env->legal, env->E, env->flags, actions, rewards, dones, env->wdl,
-                                   env->rays, rng_of(env), ply0);
+                launch_k((k_ply_rand<N, RAYS_MATH>), dim3(grid_for(env->E)), block, 0, st, env->boards,
+                         env->meta, env->legal, env->E, env->flags, actions, rewards, dones, env->wdl,
+                         env->rays, rng_of(env), ply0);
             else
-                hipLaunchKernelGGL((k_ply_rand<N, RAYS_HALF>), dim3(grid_for(env->E)), block, 0, st,
-                                   env->boards, env->meta, env->legal, env->E, env->flags, actions, rewards, dones,
-                                   env->wdl, env->rays, rng_of(env), ply0);
+                launch_k((k_ply_rand<N, RAYS_HALF>), dim3(grid_for(env->E)), block, 0, st,
+                         env->boards, env->meta, env->legal, env->E, env->flags, actions, rewards, dones,
+                         env->wdl, env->rays, rng_of(env), ply0);
             return;
         }
     }
@@ -116,20 +116,20 @@ void launch_k_play(int lanes_per_board, oth_env* env, int policy, int n_plies, i
             if constexpr (Geo<N>::W == 2)  // the max-ILP unit (play_rand_n.hip): 10x10 +5 %, 12x12 -4 %
                 launch_play_rand<N, OTH_POLICY_RANDOM>(env, n_plies, actions, rewards, dones, ply0, st);
             else
-                hipLaunchKernelGGL((k_play_rand_w<N>), grid, block, 0, st, env->boards, env->meta, env->legal, env->E,
-                                   env->flags, n_plies, actions, rewards, dones, env->wdl, rng_of(env, policy), ply0);
+                launch_k((k_play_rand_w<N>), grid, block, 0, st, env->boards, env->meta, env->legal, env->E,
+                         env->flags, n_plies, actions, rewards, dones, env->wdl, rng_of(env, policy), ply0);
             return;
         }
     }
     if constexpr (POL == OTH_POLICY_RANDOM || POL == OTH_POLICY_GREEDY) {
         if (actions && rewards && dones) {
-            hipLaunchKernelGGL((k_play<N, POL, Eng, true>), grid, block, 0, st, env->boards, env->meta, env->legal,
-                               env->E, env->flags, n_plies, actions, rewards, dones, env->wdl, rng_of(env, policy), ply0);
+            launch_k((k_play<N, POL, Eng, true>), grid, block, 0, st, env->boards, env->meta, env->legal,
+                     env->E, env->flags, n_plies, actions, rewards, dones, env->wdl, rng_of(env, policy), ply0);
             return;
         }
     }
-    hipLaunchKernelGGL((k_play<N, POL, Eng, false>), grid, block, 0, st, env->boards, env->meta, env->legal, env->E,
-                       env->flags, n_plies, actions, rewards, dones, env->wdl, rng_of(env, policy), ply0);
+    launch_k((k_play<N, POL, Eng, false>), grid, block, 0, st, env->boards, env->meta, env->legal, env->E,
+             env->flags, n_plies, actions, rewards, dones, env->wdl, rng_of(env, policy), ply0);
 }
 
 template <int N>
@@ -161,9 +161,9 @@ void launch_ss(oth_env* env, const float* logits, long long ld, const float* uni
     // (the tally slots oth_create sizes cover the quads' grid: one slot per block)
     if constexpr (Geo<N>::W == 1) {
         if (env->E <= OTH_SS_QUAD_MAX_E && grid_for(4LL * env->E) <= env->nslots) {
-            hipLaunchKernelGGL((k_sample_step4<N, VEC, FULL>), dim3(grid_for(4LL * env->E)), dim3(BLOCK), 0, st,
-                               env->boards, env->meta, env->legal, env->E, env->flags, logits, ld, uniforms, counter,
-                               mode, actions, log_probs, entropy, rewards, dones, env->wdl, rng_of(env), ply);
+            launch_k((k_sample_step4<N, VEC, FULL>), dim3(grid_for(4LL * env->E)), dim3(BLOCK), 0, st,
+                     env->boards, env->meta, env->legal, env->E, env->flags, logits, ld, uniforms, counter,
+                     mode, actions, log_probs, entropy, rewards, dones, env->wdl, rng_of(env), ply);
             return;
         }
     }
@@ -176,18 +176,18 @@ void launch_ss(oth_env* env, const float* logits, long long ld, const float* uni
     constexpr bool PAIR2 = Geo<N>::W == 2;
     if constexpr (PAIR1 || PAIR2) {
         if (PAIR1 || VEC || env->E <= OTH_SS_PAIR_W_MAX_E) {
-            hipLaunchKernelGGL((k_sample_step2<N, VEC, FULL>), dim3(grid_for(2LL * env->E)), dim3(BLOCK), 0, st,
-                               env->boards, env->meta, env->legal, env->E, env->flags, logits, ld, uniforms, counter,
-                               mode, actions, log_probs, entropy, rewards, dones, env->wdl, rng_of(env), ply);
+            launch_k((k_sample_step2<N, VEC, FULL>), dim3(grid_for(2LL * env->E)), dim3(BLOCK), 0, st,
+                     env->boards, env->meta, env->legal, env->E, env->flags, logits, ld, uniforms, counter,
+                     mode, actions, log_probs, entropy, rewards, dones, env->wdl, rng_of(env), ply);
             return;
         }
     }
     // one lane samples one board (oth_ms::sample_lane) for boards of <= 2 words
     constexpr bool ONE = Geo<N>::W <= 2;
     const long long lanes = ONE ? (long long)env->E : ((long long)env->E + G - 1) / G * G;
-    hipLaunchKernelGGL((k_sample_step<N, G, VEC, FULL, ONE>), dim3(grid_for(lanes)), dim3(BLOCK), 0, st, env->boards,
-                       env->meta, env->legal, env->E, env->flags, logits, ld, uniforms, counter, mode, actions,
-                       log_probs, entropy, rewards, dones, env->wdl, rng_of(env), ply);
+    launch_k((k_sample_step<N, G, VEC, FULL, ONE>), dim3(grid_for(lanes)), dim3(BLOCK), 0, st, env->boards,
+             env->meta, env->legal, env->E, env->flags, logits, ld, uniforms, counter, mode, actions,
+             log_probs, entropy, rewards, dones, env->wdl, rng_of(env), ply);
 }
 
 // the sampler's lanes per board: k_masked's choice for the board's word count
@@ -219,8 +219,8 @@ int launch_reset_vs(oth_env* env, int policy, const int8_t* prot, const uint8_t*
                     hipStream_t st) {
     return with_policy(policy, [&](auto PC) {
         constexpr int POL = decltype(PC)::value;
-        hipLaunchKernelGGL((k_reset_vs<N, POL>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards, env->meta,
-                           env->legal, env->E, env->flags, prot, mask, rng_of(env, policy), call);
+        launch_k((k_reset_vs<N, POL>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards, env->meta,
+                 env->legal, env->E, env->flags, prot, mask, rng_of(env, policy), call);
         return after_launch("oth_reset_vs");
     });
 }
@@ -233,13 +233,13 @@ int launch_step_vs(oth_env* env, int policy, const int32_t* actions, const int8_
         // one-word boards against a random or greedy opponent: k_step_vs1 (ply.hpp;
         // 65,536 8x8 boards 16-19 % less per call, profiles/r04/vs/)
         if constexpr (Geo<N>::W == 1 && (POL == OTH_POLICY_RANDOM || POL == OTH_POLICY_GREEDY))
-            hipLaunchKernelGGL((k_step_vs1<N, POL>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards,
-                               env->meta, env->legal, env->E, env->flags, actions, prot, rewards, dones, plies,
-                               env->wdl, env->wdl_vs, rng_of(env, policy), call);
+            launch_k((k_step_vs1<N, POL>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards,
+                     env->meta, env->legal, env->E, env->flags, actions, prot, rewards, dones, plies,
+                     env->wdl, env->wdl_vs, rng_of(env, policy), call);
         else
-            hipLaunchKernelGGL((k_step_vs<N, POL>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards,
-                               env->meta, env->legal, env->E, env->flags, actions, prot, rewards, dones, plies,
-                               env->wdl, env->wdl_vs, rng_of(env, policy), call);
+            launch_k((k_step_vs<N, POL>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards,
+                     env->meta, env->legal, env->E, env->flags, actions, prot, rewards, dones, plies,
+                     env->wdl, env->wdl_vs, rng_of(env, policy), call);
         return after_launch("oth_step_vs");
     });
 }
@@ -249,15 +249,15 @@ int launch_policy_actions(oth_env* env, int policy, int32_t* out, hipStream_t st
     return with_policy(policy, [&](auto PC) {
         constexpr int POL = decltype(PC)::value;
         if constexpr (POL != OTH_POLICY_RANDOM)
-            hipLaunchKernelGGL((k_policy_actions<N, POL>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards,
-                               env->meta, env->legal, env->E, out, rng_of(env, policy).depth);
+            launch_k((k_policy_actions<N, POL>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards,
+                     env->meta, env->legal, env->E, out, rng_of(env, policy).depth);
         return after_launch("oth_policy_actions");
     });
 }
 
 template <int N>
 int launch_legal_moves(int n, const uint64_t* mover, const uint64_t* opp, uint64_t* out, hipStream_t st) {
-    hipLaunchKernelGGL(k_legal_moves<N>, dim3(grid_for(n)), dim3(BLOCK), 0, st, mover, opp, out, n);
+    launch_k(k_legal_moves<N>, dim3(grid_for(n)), dim3(BLOCK), 0, st, mover, opp, out, n);
     return after_launch("oth_legal_moves");
 }
 
@@ -274,24 +274,24 @@ void launch_observe_bpw(oth_env* env, int layout, T* o, hipStream_t st) {
     const dim3 gw(grid_for(((long long)env->E + BPW - 1) / BPW * 64));
     switch (layout) {
         case OTH_OBS_BOARD:
-            hipLaunchKernelGGL((k_observe_w<N, OTH_OBS_BOARD, T, BPW>), gw, dim3(BLOCK), 0, st, env->boards,
-                               env->meta, env->legal, env->E, o);
+            launch_k((k_observe_w<N, OTH_OBS_BOARD, T, BPW>), gw, dim3(BLOCK), 0, st, env->boards,
+                     env->meta, env->legal, env->E, o);
             break;
         case OTH_OBS_BOARD_LEGAL:
-            hipLaunchKernelGGL((k_observe_w<N, OTH_OBS_BOARD_LEGAL, T, BPW>), gw, dim3(BLOCK), 0, st, env->boards,
-                               env->meta, env->legal, env->E, o);
+            launch_k((k_observe_w<N, OTH_OBS_BOARD_LEGAL, T, BPW>), gw, dim3(BLOCK), 0, st, env->boards,
+                     env->meta, env->legal, env->E, o);
             break;
         case OTH_OBS_MAKE_STATE:
-            hipLaunchKernelGGL((k_observe_w<N, OTH_OBS_MAKE_STATE, T, BPW>), gw, dim3(BLOCK), 0, st, env->boards,
-                               env->meta, env->legal, env->E, o);
+            launch_k((k_observe_w<N, OTH_OBS_MAKE_STATE, T, BPW>), gw, dim3(BLOCK), 0, st, env->boards,
+                     env->meta, env->legal, env->E, o);
             break;
         case OTH_OBS_ABSOLUTE:
-            hipLaunchKernelGGL((k_observe_w<N, OTH_OBS_ABSOLUTE, T, BPW>), gw, dim3(BLOCK), 0, st, env->boards,
-                               env->meta, env->legal, env->E, o);
+            launch_k((k_observe_w<N, OTH_OBS_ABSOLUTE, T, BPW>), gw, dim3(BLOCK), 0, st, env->boards,
+                     env->meta, env->legal, env->E, o);
             break;
         default:
-            hipLaunchKernelGGL((k_observe_w<N, OTH_OBS_LEGAL, T, BPW>), gw, dim3(BLOCK), 0, st, env->boards,
-                               env->meta, env->legal, env->E, o);
+            launch_k((k_observe_w<N, OTH_OBS_LEGAL, T, BPW>), gw, dim3(BLOCK), 0, st, env->boards,
+                     env->meta, env->legal, env->E, o);
             break;
     }
 }
@@ -323,21 +323,21 @@ int launch_observe(oth_env* env, int layout, int dtype, void* out, hipStream_t s
     }
     int grid = grid_for(total);
     if (grid > 65536) grid = 65536;
-    hipLaunchKernelGGL(k_observe<N>, dim3(grid), dim3(BLOCK), 0, st, env->boards, env->meta, env->legal, env->E,
-                       layout, dtype, out);
+    launch_k(k_observe<N>, dim3(grid), dim3(BLOCK), 0, st, env->boards, env->meta, env->legal, env->E,
+             layout, dtype, out);
     return after_launch("oth_observe");
 }
 
 template <int N>
 int launch_set_turn(oth_env* env, int turn, const uint8_t* mask, hipStream_t st) {
-    hipLaunchKernelGGL(k_set_turn<N>, dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards, env->meta, env->legal,
-                       env->E, turn, mask);
+    launch_k(k_set_turn<N>, dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards, env->meta, env->legal,
+             env->E, turn, mask);
     return after_launch("oth_set_player_turn");
 }
 
 template <int N>
 int launch_count(oth_env* env, int32_t* out, hipStream_t st) {
-    hipLaunchKernelGGL(k_count<N>, dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards, env->E, out);
+    launch_k(k_count<N>, dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards, env->E, out);
     return after_launch("oth_count_disks");
 }
 

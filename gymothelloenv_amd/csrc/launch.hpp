@@ -5,6 +5,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <tuple>
+#include <utility>
+
 #include "othello_mi355x.h"
 
 // one-word boards: oth_env::rays holds the 8 x 64-word ray table, then the sel8 table
@@ -45,7 +48,23 @@ namespace oth_host {
 // error reporting (capi.hip): set the thread's oth_last_error() and return the code
 int fail(int code, const char* msg);
 int hip_fail(hipError_t err, const char* where);
+// the status of the launches since the last after_launch (hipGetLastError too)
 int after_launch(const char* what);
+void note_launch(hipError_t err);
+
+// Every kernel launch of the C ABI: hipLaunchKernel on the kernel's host stub with
+// the arguments converted to the kernel's parameter types, its status kept for
+// after_launch.  From C, oth_step costs 3.04 us per call this way against 3.79
+// through hipLaunchKernelGGL (same box, tools/launch_cost.hip; profiles/r04/lc/).
+template <typename... P, typename... A>
+inline void launch_k(void (*k)(P...), dim3 grid, dim3 block, size_t shmem, hipStream_t st, A&&... a) {
+    static_assert(sizeof...(P) == sizeof...(A), "one argument per kernel parameter");
+    std::tuple<P...> args{static_cast<P>(std::forward<A>(a))...};
+    std::apply([&](auto&... x) {
+        void* ptrs[] = {static_cast<void*>(&x)...};
+        note_launch(hipLaunchKernel(reinterpret_cast<const void*>(k), grid, block, ptrs, shmem, st));
+    }, args);
+}
 
 // masked categorical (masked.hip), any board size
 int launch_masked(int n_board, int E, const float* logits, long long ld, const uint64_t* legal, const float* uniforms,

@@ -55,11 +55,11 @@ void launch_one(bool vec, int E, hipStream_t st, int NN, const float* logits, lo
     const long long groups = ((long long)E + BPR - 1) / BPR;
     const int grid = (int)((groups * G + MS_BLOCK - 1) / MS_BLOCK);
     if (vec)
-        hipLaunchKernelGGL((k_masked<CH, G, true, BPR, FULL>), dim3(grid), dim3(MS_BLOCK), 0, st, E, NN, logits, ld,
-                           legal, uniforms, seed, id_base, counter, counter_off, mode, actions, log_probs, entropy);
+        oth_host::launch_k((k_masked<CH, G, true, BPR, FULL>), dim3(grid), dim3(MS_BLOCK), 0, st, E, NN, logits, ld,
+                 legal, uniforms, seed, id_base, counter, counter_off, mode, actions, log_probs, entropy);
     else
-        hipLaunchKernelGGL((k_masked<CH, G, false, BPR, FULL>), dim3(grid), dim3(MS_BLOCK), 0, st, E, NN, logits, ld,
-                           legal, uniforms, seed, id_base, counter, counter_off, mode, actions, log_probs, entropy);
+        oth_host::launch_k((k_masked<CH, G, false, BPR, FULL>), dim3(grid), dim3(MS_BLOCK), 0, st, E, NN, logits, ld,
+                 legal, uniforms, seed, id_base, counter, counter_off, mode, actions, log_probs, entropy);
 }
 
 template <int CH, int G, int BPR>

@@ -25,11 +25,11 @@ void launch_play_rand(oth_env* env, int n_plies, int32_t* actions, int32_t* rewa
     const dim3 grid((unsigned)(((long long)env->E + BLOCK - 1) / BLOCK)), block(BLOCK);
     const Rng rng{env->seed, env->id_base, env->init_rand, env->cur_off};
     if constexpr (Geo<N>::W == 1)
-        hipLaunchKernelGGL((k_play_rand<N, POL>), grid, block, 0, st, env->boards, env->meta, env->legal, env->E,
-                           env->flags, n_plies, actions, rewards, dones, env->wdl, rng, ply0, env->rays);
+        launch_k((k_play_rand<N, POL>), grid, block, 0, st, env->boards, env->meta, env->legal, env->E,
+                 env->flags, n_plies, actions, rewards, dones, env->wdl, rng, ply0, env->rays);
     else  // random play only (k_play_rand_w)
-        hipLaunchKernelGGL((k_play_rand_w<N>), grid, block, 0, st, env->boards, env->meta, env->legal, env->E,
-                           env->flags, n_plies, actions, rewards, dones, env->wdl, rng, ply0);
+        launch_k((k_play_rand_w<N>), grid, block, 0, st, env->boards, env->meta, env->legal, env->E,
+                 env->flags, n_plies, actions, rewards, dones, env->wdl, rng, ply0);
 }
 
 template void launch_play_rand<OTH_N, OTH_POLICY_RANDOM>(oth_env*, int, int32_t*, int32_t*, uint8_t*, uint64_t,

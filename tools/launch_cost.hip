@@ -40,6 +40,32 @@ int main(int argc, char** argv) {
     double t2 = now_us();
     printf("{\"case\": \"empty\", \"host_us_per_launch\": %.3f, \"drain_us\": %.1f, \"total_us_per_launch\": %.3f}\n",
            (t1 - t0) / K, t2 - t1, (t2 - t0) / K);
+    // the host calls around a launch in the C ABI: hipGetDevice (use_device) and
+    // hipGetLastError (after_launch), and hipLaunchKernel returning its status
+    {
+        int dev = 0;
+        double a0 = now_us();
+        for (int i = 0; i < K; ++i) (void)hipGetDevice(&dev);
+        double a1 = now_us();
+        for (int i = 0; i < K; ++i) (void)hipGetLastError();
+        double a2 = now_us();
+        void* kargs[] = {nullptr};
+        int* nullp = nullptr;
+        kargs[0] = &nullp;
+        for (int i = 0; i < K; ++i)
+            (void)hipLaunchKernel((const void*)k_empty, dim3(E / 256), dim3(256), kargs, 0, st);
+        double a3 = now_us();
+        if (hipStreamSynchronize(st) != hipSuccess) return 2;
+        for (int i = 0; i < K; ++i) {
+            hipLaunchKernelGGL(k_empty, dim3(E / 256), dim3(256), 0, st, nullptr);
+            (void)hipGetLastError();
+        }
+        double a4 = now_us();
+        if (hipStreamSynchronize(st) != hipSuccess) return 2;
+        printf("{\"case\": \"host_calls\", \"hipGetDevice_us\": %.3f, \"hipGetLastError_us\": %.3f, "
+               "\"hipLaunchKernel_us\": %.3f, \"launchGGL_plus_getlasterror_us\": %.3f}\n",
+               (a1 - a0) / K, (a2 - a1) / K, (a3 - a2) / K, (a4 - a3) / K);
+    }
     if (argc < 2) return 0;
     void* so = dlopen(argv[1], RTLD_NOW);
     if (!so) {
