@@ -232,6 +232,41 @@ __device__ __forceinline__ void fill_rays(uint64_t* rays) {
     if (SYNC) __syncthreads();
 }
 
+// Without a table: the rays of square s toward higher squares (E, S, SE, SW)
+// as one shifted constant each -- the ray from square 0 (or row 0's squares
+// 1 .. N-1 for E) moved to s -- with the squares that wrapped past the board's
+// right (E, SE) or left (SW) edge masked off by column.
+template <int N>
+struct RayMath {
+    static constexpr uint64_t sum_steps(int step, int k0, int k1) {
+        uint64_t x = 0;
+        for (int k = k0; k <= k1; ++k) x |= 1ull << (k * step);
+        return x;
+    }
+    static constexpr uint64_t BD = Geo<N>::BOARD.w[0];
+    static constexpr uint64_t ROW1 = sum_steps(N, 0, N - 1);      // column 0 of every row
+    static constexpr uint64_t EAST = ((1ull << N) - 1) & ~1ull;    // squares 1 .. N-1 of row 0
+    static constexpr uint64_t COL = sum_steps(N, 1, N - 1);       // S from square 0
+    static constexpr uint64_t DIAG = sum_steps(N + 1, 1, N - 1);  // SE from square 0
+    static constexpr uint64_t ANTI = sum_steps(N - 1, 1, N - 1);  // SW from square N-1, moved to square 0
+    // square s of the board turned by 180 degrees, for any s < 64: an invalid
+    // action's square may lie past N*N - 1 on boards of N < 8, so the result is
+    // kept below 64 (every shift count of up() stays defined; the caller masks
+    // the flips of an invalid action)
+    __device__ __forceinline__ static uint32_t turned(uint32_t s) {
+        return N == 8 ? N * N - 1 - s : (N * N - 1 - s) & 63u;
+    }
+    __device__ __forceinline__ static void up(uint32_t s, uint32_t c, uint64_t* ray) {
+        const uint32_t row = (1u << N) - 1u;
+        const uint64_t gt = ROW1 * (uint64_t)((row << (c + 1)) & row);  // columns > c of every row
+        const uint64_t lt = ROW1 * (uint64_t)((1u << c) - 1u);           // columns < c
+        ray[0] = (EAST << s) & gt;
+        ray[1] = (COL << s) & BD;
+        ray[2] = (DIAG << s) & gt & BD;
+        ray[3] = (ANTI << s) & lt & BD;
+    }
+};
+
 // Fills<N>: flips from the ray tables and the legal scan's fills.  legal_moves' axis scans
 // compute, for the side to move, the fills t(dir) = opponent discs reachable
 // from an own disc through contiguous opponent discs stepping in direction dir
@@ -266,6 +301,9 @@ struct Fills {
     }
     __device__ __forceinline__ BB<1> flip(const BB<1>&, const BB<1>&, int a) const {
         const uint64_t* r = rays + a;
+        // (the rays computed by RayMath instead of read from the LDS table: 8x8
+        // 0.671 -> 0.696 us per ply, greedy +2.8 %, 6x6 +3.3 %: +38 VALU per ply cost
+        // more than the LDS round trip they remove; profiles/r04/fm/ab.jsonl)
         uint64_t f = 0;
 #pragma unroll
         for (int d = 0; d < 4; ++d) {  // toward higher squares: cap = lowest ray square outside the fill
