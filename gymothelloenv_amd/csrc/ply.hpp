@@ -403,6 +403,9 @@ __global__ __launch_bounds__(BLOCK) void k_step_vs1(uint64_t* __restrict__ board
             step1<N, RAYS_MATH, KEEP>(B, Wt, L, m, a, valid, flags, no_table, r, d, win, 0, t);
             have_t = true;
         };
+        // (keeping the Philox block across a chain of opponent plies instead of
+        // action_draw's block per ply measured +-0: 15.20 -> 15.09 us per call with a
+        // random opponent, 15.03 -> 15.08 greedy; profiles/r04/vs/ab_vs_block.jsonl)
         auto random_pick = [&](uint64_t g) __attribute__((always_inline)) {  // random_action: -1 without a move
             const int n = popc64(L);
             return n ? select64(L, scale_index(action_draw(rng.seed, id, g), n)) : -1;
