@@ -1232,7 +1232,11 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
                 // an opening ply's draw is word g % 4 of Philox block g / 4 (action_draw's
                 // value); the block is computed once per group of four plies, at the first
                 // ply where some board of the wave has opening plies left (uniform branch):
-                // one Philox evaluation per 4 plies instead of one per ply
+                // one Philox evaluation per 4 plies instead of one per ply.  The same for
+                // the auto-reset's opening-length draw (a wave-wide block per group, the
+                // draw spec changed to block form) measured 3-4 % slower: a wave's greedy
+                // games run almost in step, so few plies see a game end
+                // (profiles/r04/oblk/)
                 U4 blk{0u, 0u, 0u, 0u};
                 uint64_t held = ~0ull;  // the block in blk (wave-uniform)
                 for (int p = 0; p < plies; ++p) {
