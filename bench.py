@@ -167,6 +167,29 @@ def load_pmc(workload):
     return None
 
 
+def pmc_ref(workload, plies=1):
+    """A compact reference to the committed PMC record of `workload` (its
+    profiles/ path, the HBM bytes and VALU wave-instructions per launch, VALU
+    per wave and ply), or None: the bench line names the record, it does not
+    inline it."""
+    rec = load_pmc(workload)
+    if not rec:
+        return None
+    out = {"source": rec.get("source"), "hbm_bytes_per_launch": _r(rec.get("hbm_bytes_per_launch"))}
+    if rec.get("valu_insts_per_launch") and rec.get("waves_per_launch"):
+        out["valu_per_wave_ply"] = _r(rec["valu_insts_per_launch"] / rec["waves_per_launch"] / plies)
+    return out
+
+
+def _r(x, digits=4):
+    """x to `digits` significant digits (keeps the one JSON line short)."""
+    if x is None or isinstance(x, (bool, str)):
+        return x
+    if isinstance(x, int):
+        return x
+    return float("%.*g" % (digits, x))
+
+
 def play_kernel_name(n, policy, record):
     """The kernel oth_step_policy launches for this configuration (kernels_n.hip
     launch_k_play): the restructured auto-reset kernels when every per-ply
@@ -366,7 +389,8 @@ def main(argv=None):
 
     side = {}
     if not args.no_side and world == 1 and rank == 0:
-        side = side_measurements(env.env, args.policy, E, n, W, dev, stream)
+        side = side_measurements(env.env, args.policy, E, n, W, dev, stream, P=P, bufs=(acts, rews, dns),
+                                 burst_us=kern_ms * 1e3 / args.steps)
 
     if rank == 0:
         out = make_record(args, world, G, E, P, n, record, wall_max, kern_ms, wdl_total, solo=solo,
@@ -374,6 +398,8 @@ def main(argv=None):
         out.update(side)
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, n)
+        if side:
+            out["side_summary"] = side_summary(side, out)  # last: a truncated tail still shows it
         print(json.dumps(out), flush=True)
     env.close()
     if world > 1:
@@ -428,7 +454,8 @@ def make_record(args, world, G, E, P, n, record, wall_max, kern_ms, wdl_total, s
                    "global_boards": G, "board_size": n, "plies_per_step": P,
                    "env_steps_per_step": G * P, "policy": args.policy, "per_ply_outputs_stored": record,
                    "parallelism": "dp%d (independent shards, W/D/L all-gather only)" % world},
-        "roofline": {"bound": "hbm", "limiter": "integer VALU issue (see valu)",
+        "roofline": {"bound": "valu-issue", "limiter": "integer VALU issue at one wave per SIMD (see valu); "
+                                                         "achieved / frac are against HBM",
                      "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS if achieved else None,
                      "achieved_kind": "equivalent bandwidth: SURVEY §8(d)'s algorithmic bytes over the launch time; "
@@ -532,6 +559,148 @@ def step_external(E, n, dev, stream, plies=64):
             "replay_equals_recording": same}
 
 
+def _graph_us(env, start, fn, k, stream):
+    """Median of 5 replays of a HIP graph of fn(0 .. k-1) (inside a graph
+    region: fresh Philox counters every replay), each replay from the state
+    `start`; us per call."""
+    import torch
+    g = torch.cuda.CUDAGraph()
+    env.set_state(*start)
+    with torch.cuda.graph(g), env.graph_region():
+        for i in range(k):
+            fn(i)
+    reps = []
+    for _ in range(5):
+        env.set_state(*start)
+        reps.append(_time_launches(stream, lambda i: g.replay(), 1) / k)
+    del g
+    return statistics.median(reps)
+
+
+def step_observe_lines(E, n, dev, stream, plies=32):
+    """The step with its observation from one launch, against the two-launch
+    form and the parts alone, graphed (plies calls, median of 5 replays, each
+    from the same mid-game state):
+      * oth_step_observe: OthelloBaseEnv.step's (obs, reward, done) tuple
+        (othello.py:412-462) with the int64 get_observation (:363-378), replaying
+        recorded random moves;
+      * oth_sample_step_observe: the learners' ply -- Policy.act's masked sample
+        (model.py:60-99) + step + util.make_state f32 (util.py:48-74), the next
+        input of the policy network.
+    frac: SURVEY §8(d)'s 51 B per env-step plus the observation written (512 B
+    int64 board / 1,024 B f32 make_state per 8x8 board), plus the logits read
+    and the sample written (4N² + 12 B) for the learners' ply, over the time."""
+    import torch
+
+    from gymothelloenv_amd import VecOthelloEnv
+    from gymothelloenv_amd.vec_env import nwords
+    W, NN = nwords(n), n * n
+    env = VecOthelloEnv(E, board_size=n, auto_reset=True, seed=7, device=dev)
+    env.step_policy("random", n_plies=30, record=False)
+    start = env.get_state()
+    acts = env.step_policy("random", n_plies=plies)[0]
+    rew = torch.empty(E, dtype=torch.int32, device=dev)
+    don = torch.empty(E, dtype=torch.uint8, device=dev)
+    ob = torch.empty(E, n, n, dtype=torch.int64, device=dev)
+    ms = torch.empty(E, 4, n, n, dtype=torch.float32, device=dev)
+    a = torch.empty(E, dtype=torch.int32, device=dev)
+    lp = torch.empty(E, dtype=torch.float32, device=dev)
+    en = torch.empty(E, dtype=torch.float32, device=dev)
+    logits = torch.randn(E, NN, device=dev, generator=torch.Generator(device=dev).manual_seed(0))
+
+    def ss(i, obs=False):
+        return env.sample_step(logits, actions=a, log_probs=lp, entropy=en, rewards=rew, dones=don,
+                               **({"observe": "make_state", "obs": ms} if obs else {}))
+    t = {"step_board_fused": lambda i: env.step(acts[i], rewards=rew, dones=don, obs=ob),
+         "step_board_split": lambda i: (env.step(acts[i], rewards=rew, dones=don, observe=False),
+                                        env.observe("board", torch.int64, out=ob)),
+         "step_only": lambda i: env.step(acts[i], rewards=rew, dones=don, observe=False),
+         "sample_step_make_state_fused": lambda i: ss(i, True),
+         "sample_step_make_state_split": lambda i: (ss(i), env.observe("make_state", torch.float32, out=ms)),
+         "sample_step_only": lambda i: ss(i)}
+    us = {k: _graph_us(env, start, fn, plies, stream) for k, fn in t.items()}
+    env.close()
+    step_b = 40 * W + 11
+    b_board = E * (step_b + 8 * NN)
+    b_ms = E * (4 * NN + 12 + step_b + 4 * 4 * NN)
+
+    def frac(b, u):
+        return _r(b / (u * 1e-6) / 1e9 / HBM_PEAK_GBPS)
+    return {"boards": E, "board_size": n,
+            "us": {k: _r(v) for k, v in us.items()},
+            "step_board": {"kernel": "k_ply_step_obs<%d>" % n if W == 1 else "k_step<%d> + k_observe_w" % n,
+                           "us_per_ply": _r(us["step_board_fused"]),
+                           "two_launch_us": _r(us["step_board_split"]),
+                           "algorithmic_bytes_per_board": step_b + 8 * NN,
+                           "frac": frac(b_board, us["step_board_fused"])},
+            "sample_step_make_state": {"kernel": "k_sample_step2<%d> + obs tail" % n,
+                                       "us_per_ply": _r(us["sample_step_make_state_fused"]),
+                                       "two_launch_us": _r(us["sample_step_make_state_split"]),
+                                       "algorithmic_bytes_per_board": 4 * NN + 12 + step_b + 16 * NN,
+                                       "frac": frac(b_ms, us["sample_step_make_state_fused"])},
+            "timing": "HIP graph of %d calls from one mid-game state, median of 5 replays" % plies}
+
+
+def sustained_line(env, policy, P, acts, rews, dns, stream, burst_launch_us, seconds=2.0):
+    """The headline launch back to back for about `seconds` (against the timed
+    region's short burst, which a clock that drops under sustained load would
+    flatter, MI355X_MICROARCH.md 'DVFS give-back').  The effective clock of
+    the same sustained run is measured by rocprofv3's GRBM_GUI_ACTIVE in its own
+    pass (tools/gpu_sustained_clock.sh) and referenced here."""
+    k = max(20, int(seconds / (burst_launch_us * 1e-6)))
+    us = _time_launches(stream, lambda i: env.step_policy(policy, n_plies=P, actions=acts, rewards=rews,
+                                                          dones=dns), k)
+    n = env.board_size
+    rec = load_pmc("sustained-%s-play-%dx%d-E%d-P%d" % (policy, n, n, env.num_envs, P))
+    return {"launches": k, "seconds": _r(k * us * 1e-6), "avg_launch_us": _r(us),
+            "value": _r(env.num_envs * P / (us * 1e-6)), "unit": "env-steps/s",
+            "vs_burst": _r(burst_launch_us / us),
+            "effective_clock_ghz": _r(rec.get("effective_clock_ghz")) if rec else None,
+            "clock_source": rec.get("source") if rec else None}
+
+
+def side_summary(side, out):
+    """The side lines' headline numbers in one compact object, printed LAST on
+    the line (a truncated tail still holds them): us per ply (or call), frac of
+    HBM, VALU per wave-ply from the committed PMC records."""
+    summ = {}
+
+    def pm(x):
+        p = ((x.get("roofline") or {}).get("pmc") or {})
+        return p.get("valu_per_wave_ply")
+    c = side.get("configs", {})
+    for x in c.get("config3_greedy", []):
+        summ["config3_greedy_P%d" % x["plies_per_launch"]] = {
+            "us_per_ply": _r(x["us_per_ply"]), "frac": _r(x["roofline"]["frac"]), "valu_per_wave_ply": pm(x)}
+    for x in c.get("config5_random", []):
+        summ["config5_random_%dx%d" % (x["board_size"], x["board_size"])] = {
+            "us_per_ply": _r(x["us_per_ply"]), "frac": _r(x["roofline"]["frac"]), "valu_per_wave_ply": pm(x)}
+    if c.get("config1_single_board"):
+        summ["config1_single_board"] = {"us_per_step": _r(c["config1_single_board"]["us_per_step"])}
+    for x in side.get("step_external", []):
+        summ["step_external_E%d" % x["boards"]] = {"us_per_ply": _r(x["avg_launch_us"]),
+                                                   "eager_us": _r(x["eager_avg_launch_us"]),
+                                                   "frac": _r(x["roofline"]["frac"])}
+    so = side.get("step_observe")
+    if so:
+        for k in ("step_board", "sample_step_make_state"):
+            summ[k] = {"us_per_ply": so[k]["us_per_ply"], "two_launch_us": so[k]["two_launch_us"],
+                       "frac": so[k]["frac"]}
+        summ["sample_step"] = {"us_per_ply": so["us"]["sample_step_only"]}
+    for x in side.get("othello_env_vs", []):
+        summ["othello_env_vs_" + x["opponent"]] = {"us_per_call": _r(x["us_per_call"]),
+                                                   "env_steps_per_s": _r(x["env_steps_per_s"])}
+    for x in side.get("observe", []):
+        summ[x["workload"]] = {"us": _r(x["avg_launch_us"]), "frac": _r(x["roofline"]["frac"])}
+    if side.get("sustained"):
+        summ["sustained"] = {k: side["sustained"][k] for k in ("seconds", "avg_launch_us", "vs_burst",
+                                                                 "effective_clock_ghz")}
+    v = (out.get("roofline") or {}).get("valu") or {}
+    summ["headline"] = {"us_per_launch": _r(out["roofline"]["avg_launch_us"]), "frac": _r(out["roofline"]["frac"]),
+                        "valu_per_board_ply": _r(v.get("valu_insts_per_board_ply"))}
+    return summ
+
+
 def vs_line(E, n, dev, stream, calls=64, opponent="random"):
     """OthelloEnv's turn loop on the device (othello.py:151-200; oth_reset_vs /
     oth_step_vs): a greedy protagonist (oth_policy_actions, GreedyPolicy
@@ -565,7 +734,7 @@ def vs_line(E, n, dev, stream, calls=64, opponent="random"):
     applied = int(sum(int(p.sum().item()) for p in plies))  # plies of the last replay
     wdl = [int(x) for x in env.counts_vs()]
     env.close()
-    return {"workload": "othello-env-vs-%s-8x8-E%d" % (opponent, E), "boards": E,
+    return {"workload": "othello-env-vs-%s-%dx%d-E%d" % (opponent, n, n, E), "boards": E, "opponent": opponent,
             "kernels": "k_policy_actions<greedy> + k_step_vs%s<%s>" % ("1" if n <= 8 else "", opponent),
             "us_per_call": us,
             "plies_per_call": applied / calls, "env_steps_per_s": applied / calls / (us * 1e-6),
@@ -631,7 +800,7 @@ def play_line(policy, n, E, P, init_rand, dev, stream, launches=20, warm=3):
             "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": gbs / HBM_PEAK_GBPS, "algorithmic_bytes_per_env_step": bps,
                          "fused_bytes_per_launch": fused_bytes_per_launch(E, W, P),
-                         "pmc": load_pmc(workload)}}
+                         "pmc": pmc_ref(workload, P)}}
 
 
 def observe_bytes(n, E, layout, esize):
@@ -674,7 +843,7 @@ def observe_lines(n, sizes, dev, stream, launches=50):
                         "timing": "HIP graph of %d launches, median of 5 replays" % launches,
                         "roofline": {"bound": "hbm", "achieved": b / (us * 1e-6) / 1e9, "peak": HBM_PEAK_GBPS,
                                      "unit": "GB/s", "frac": b / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS,
-                                     "pmc": load_pmc(workload)}})
+                                     "pmc": pmc_ref(workload)}})
             del buf
         env.close()
     return out
@@ -715,7 +884,7 @@ def config1_line(dev, seconds=0.5):
                     "throughput"}
 
 
-def side_measurements(env, policy, E, n, W, dev, stream):
+def side_measurements(env, policy, E, n, W, dev, stream, P=None, bufs=None, burst_us=None):
     """Beside the headline (never `value`): the per-step paths with the state
     through HBM every ply -- oth_step with external actions (`step_external`)
     and one-ply launches of the policy (`single_ply_launches`) -- at config 2's
@@ -727,6 +896,7 @@ def side_measurements(env, policy, E, n, W, dev, stream):
 
     from gymothelloenv_amd import VecOthelloEnv
     out = {"step_external": [step_external(Eb, n, dev, stream) for Eb in (E, 1048576)]}
+    out["step_observe"] = step_observe_lines(E, n, dev, stream)
     # BASELINE configs 3 (greedy, 8x8) and 5 (random, 6x6 and 10x10) at their stated 65,536 boards
     out["configs"] = {"config3_greedy": [play_line("greedy", 8, CONFIG2_BOARDS, P, 10, dev, stream)
                                          for P in (10, 100)],
@@ -769,6 +939,8 @@ def side_measurements(env, policy, E, n, W, dev, stream):
                             "algorithmic_bytes_per_launch": bm, "achieved_GBps": bm / (us * 1e-6) / 1e9,
                             "frac_hbm_peak": bm / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS}
     del logits, legal, outs
+    if bufs is not None and burst_us:
+        out["sustained"] = sustained_line(env, policy, P, *bufs, stream, burst_us)
     return out
 
 

@@ -38,6 +38,28 @@ OTH_MASKED_FULL_ENTROPY = 4
 OTH_GRAPH_SLOTS = 64
 OTH_GRAPH_COUNTER_SHIFT = 40
 
+OTH_RECORD_MAX_WORDS = 4
+OTH_RECORD_MAX_SQUARES = 256
+
+
+class OthRecord(ctypes.Structure):
+    """struct oth_record (include/othello_mi355x.h): one board as oth_step_sync
+    leaves it in the handle's mapped host buffer."""
+    _fields_ = [("black", ctypes.c_uint64 * OTH_RECORD_MAX_WORDS),
+                ("white", ctypes.c_uint64 * OTH_RECORD_MAX_WORDS),
+                ("legal", ctypes.c_uint64 * OTH_RECORD_MAX_WORDS),
+                ("seq", ctypes.c_uint32),
+                ("meta", ctypes.c_uint16),
+                ("done", ctypes.c_uint8),
+                ("planes", ctypes.c_uint8),
+                ("reward", ctypes.c_int32),
+                ("white_cnt", ctypes.c_int32),
+                ("black_cnt", ctypes.c_int32),
+                ("greedy", ctypes.c_int32),
+                ("obs", ctypes.c_int8 * (2 * OTH_RECORD_MAX_SQUARES)),
+                ("board_state", ctypes.c_int8 * OTH_RECORD_MAX_SQUARES)]
+
+
 # every symbol include/othello_mi355x.h declares: (restype, argtypes)
 _P = ctypes.c_void_p
 _I32, _U32, _U64, _I64 = ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int64
@@ -46,6 +68,8 @@ SIGNATURES = {
     "oth_destroy": (_I32, [_P]),
     "oth_reset": (_I32, [_P, _P, _P]),
     "oth_step": (_I32, [_P, _P, _P, _P, _P]),
+    "oth_step_observe": (_I32, [_P, _P, _P, _P, _I32, _I32, _P, _P]),
+    "oth_step_sync": (_I32, [_P, _I32, _I32, _I32, _I32, ctypes.POINTER(_P), _P]),
     "oth_step_policy": (_I32, [_P, _I32, _I32, _P, _P, _P, _P]),
     "oth_reset_vs": (_I32, [_P, _I32, _P, _P, _P]),
     "oth_step_vs": (_I32, [_P, _I32, _P, _P, _P, _P, _P, _P]),
@@ -63,6 +87,7 @@ SIGNATURES = {
     "oth_masked_sample": (_I32, [_I32, _I32, _P, _I64, _P, _P, _U64, _U32, _U64, _I32, _P, _P, _P, _P]),
     "oth_sample_actions": (_I32, [_P, _P, _I64, _P, _U64, _I32, _P, _P, _P, _P]),
     "oth_sample_step": (_I32, [_P, _P, _I64, _P, _U64, _I32, _P, _P, _P, _P, _P, _P]),
+    "oth_sample_step_observe": (_I32, [_P, _P, _I64, _P, _U64, _I32, _P, _P, _P, _P, _P, _I32, _I32, _P, _P]),
     "oth_ply_counter": (_U64, [_P]),
     "oth_set_ply_counter": (_I32, [_P, _U64]),
     "oth_graph_begin": (_I32, [_P, _P]),

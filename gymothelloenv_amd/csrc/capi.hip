@@ -206,6 +206,7 @@ int oth_destroy(oth_env* env) {
     if (env->wdl_vs) (void)hipFree(env->wdl_vs);
     if (env->ctr_slots) (void)hipFree(env->ctr_slots);
     if (env->rays) (void)hipFree(env->rays);
+    if (env->rec_host) (void)hipHostFree(env->rec_host);
     delete env;
     return OTH_OK;
 }
@@ -222,6 +223,66 @@ int oth_step(oth_env* env, const int32_t* actions, int32_t* rewards, uint8_t* do
     return with_n(env->n, [&](auto NC) {
         return launch_step<decltype(NC)::value>(env, actions, rewards, dones, ply, (hipStream_t)stream);
     });
+}
+
+int oth_step_observe(oth_env* env, const int32_t* actions, int32_t* rewards, uint8_t* dones, int32_t layout,
+                     int32_t dtype, void* obs, oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    if (!actions || !obs) return fail(OTH_EINVAL, "actions / obs is NULL");
+    if (layout < OTH_OBS_BOARD || layout > OTH_OBS_LEGAL) return fail(OTH_EINVAL, "unknown layout");
+    if (dtype < OTH_I8 || dtype > OTH_F64) return fail(OTH_EINVAL, "unknown dtype");
+    const uint64_t ply = env->ply++;
+    return with_n(env->n, [&](auto NC) {
+        return launch_step_observe<decltype(NC)::value>(env, actions, rewards, dones, layout, dtype, obs, ply,
+                                                        (hipStream_t)stream);
+    });
+}
+
+int oth_step_sync(oth_env* env, int32_t board, int32_t step, int32_t action, int32_t layout, const oth_record** out,
+                  oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    if (!out) return fail(OTH_EINVAL, "out is NULL");
+    if (board < 0 || board >= env->E) return fail(OTH_EINVAL, "board out of range");
+    if (layout != OTH_OBS_BOARD && layout != OTH_OBS_BOARD_LEGAL)
+        return fail(OTH_EINVAL, "layout must be OTH_OBS_BOARD or OTH_OBS_BOARD_LEGAL");
+    if (!env->rec_host) {  // mapped, coherent pinned host memory: the kernel's stores land in it directly
+        void* h = nullptr;
+        OTH_HIP(hipHostMalloc(&h, sizeof(oth_record), hipHostMallocMapped | hipHostMallocCoherent));
+        memset(h, 0, sizeof(oth_record));
+        void* d = nullptr;
+        const hipError_t err = hipHostGetDevicePointer(&d, h, 0);
+        if (err != hipSuccess) {
+            (void)hipHostFree(h);
+            return hip_fail(err, "oth_step_sync: hipHostGetDevicePointer");
+        }
+        env->rec_host = static_cast<oth_record*>(h);
+        env->rec_dev = static_cast<oth_record*>(d);
+        env->rec_seq = 0;
+    }
+    const uint32_t seq = ++env->rec_seq;
+    const uint64_t ply = step ? env->ply++ : env->ply;
+    const int rc = with_n(env->n, [&](auto NC) {
+        return launch_record<decltype(NC)::value>(env, board, step ? 1 : 0, action,
+                                                  layout == OTH_OBS_BOARD_LEGAL ? 2 : 1, ply, (hipStream_t)stream);
+    });
+    if (rc) return rc;
+    // wait for the sequence number (the kernel writes it last, behind a system-scope
+    // fence): no runtime synchronisation on the path; after a bounded spin the
+    // stream is synchronised instead, which also reports a failed kernel
+    const volatile uint32_t* sp = &env->rec_host->seq;
+    for (int i = 0; i < (1 << 22); ++i) {
+        if (*sp == seq) {
+            __atomic_thread_fence(__ATOMIC_ACQUIRE);
+            *out = env->rec_host;
+            return OTH_OK;
+        }
+        __builtin_ia32_pause();
+    }
+    OTH_HIP(hipStreamSynchronize((hipStream_t)stream));
+    if (*sp != seq) return fail(OTH_EHIP, "oth_step_sync: the record did not arrive");
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    *out = env->rec_host;
+    return OTH_OK;
 }
 
 int oth_step_policy(oth_env* env, int32_t policy, int32_t n_plies, int32_t* actions, int32_t* rewards,
@@ -332,7 +393,26 @@ int oth_sample_step(oth_env* env, const float* logits, int64_t ld, const float* 
     const uint64_t ply = env->ply++;
     return with_n(env->n, [&](auto NC) {
         return launch_sample_step<decltype(NC)::value>(env, logits, (long long)ld, uniforms, counter, mode, actions,
-                                                       log_probs, entropy, rewards, dones, ply, (hipStream_t)stream);
+                                                       log_probs, entropy, rewards, dones, ply, -1, 0, nullptr,
+                                                       (hipStream_t)stream);
+    });
+}
+
+int oth_sample_step_observe(oth_env* env, const float* logits, int64_t ld, const float* uniforms, uint64_t counter,
+                            int32_t mode, int32_t* actions, float* log_probs, float* entropy, int32_t* rewards,
+                            uint8_t* dones, int32_t layout, int32_t dtype, void* obs, oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    if (!logits || !actions || !obs) return fail(OTH_EINVAL, "logits / actions / obs is NULL");
+    const int base = mode & ~OTH_MASKED_FULL_ENTROPY;
+    if (base != OTH_MASKED_SAMPLE && base != OTH_MASKED_MODE) return fail(OTH_EINVAL, "mode must be SAMPLE or MODE");
+    if (ld < (int64_t)env->n * env->n) return fail(OTH_EINVAL, "ld < N*N");
+    if (layout < OTH_OBS_BOARD || layout > OTH_OBS_LEGAL) return fail(OTH_EINVAL, "unknown layout");
+    if (dtype < OTH_I8 || dtype > OTH_F64) return fail(OTH_EINVAL, "unknown dtype");
+    const uint64_t ply = env->ply++;
+    return with_n(env->n, [&](auto NC) {
+        return launch_sample_step<decltype(NC)::value>(env, logits, (long long)ld, uniforms, counter, mode, actions,
+                                                       log_probs, entropy, rewards, dones, ply, layout, dtype, obs,
+                                                       (hipStream_t)stream);
     });
 }
 

@@ -1795,58 +1795,52 @@ __device__ __forceinline__ void put_quad(T* out, uint32_t q, int v0, int v1, int
     }
 }
 
-// k_observe_w: the same values as k_observe, one wave per 64
-// consecutive boards.  Each lane loads one board (coalesced), then the wave
-// streams the boards' contiguous output region -- 64 x planes x N*N/4 quads --
-// one 64-quad vector store per step, each lane taking the words of the board
-// its quad belongs to from that board's lane (ds_bpermute).  One board per
-// wave (round 2's k_observe_q, each wave waiting on its own board's loads
-// before one 1-KiB store) reached 2.6 TB/s for make_state f32 at 1,048,576
-// boards; one wave's loads feeding 64 boards' stores, 5.0 (a plain fill: 6.9).
-// BPW boards per wave (64, or 16 for small launches: four times the waves, each
-// streaming a quarter of the region, so the store streams start sooner and
-// more of them are in flight).
-template <int N, int LAYOUT, typename T, int BPW = 64>
-__global__ __launch_bounds__(BLOCK) void k_observe_w(const uint64_t* __restrict__ boards,
-                                                     const uint16_t* __restrict__ meta,
-                                                     const uint64_t* __restrict__ legal, int E, T* __restrict__ out) {
-    static_assert(BPW == 4 || BPW == 8 || BPW == 16 || BPW == 32 || BPW == 64, "boards per wave");
+template <int LAYOUT>
+constexpr int obs_planes() {
+    return LAYOUT == OTH_OBS_BOARD_LEGAL ? 2 : (LAYOUT == OTH_OBS_MAKE_STATE ? 4 : 1);
+}
+template <int LAYOUT>
+constexpr bool obs_needs_legal() {
+    return LAYOUT == OTH_OBS_BOARD_LEGAL || LAYOUT == OTH_OBS_MAKE_STATE || LAYOUT == OTH_OBS_LEGAL;
+}
+// the board facts the observation needs beside its words: bit 0 white to move,
+// bit 1 more than one legal move (util.py:55's make_state condition)
+template <int W>
+__device__ __forceinline__ uint32_t obs_flags(uint32_t m, const uint64_t (&lw)[W]) {
+    int cnt = 0;
+#pragma unroll
+    for (int k = 0; k < W; ++k) cnt += popc64(lw[k]);
+    return ((m & M_TURN_WHITE) ? 1u : 0u) | (cnt > 1 ? 2u : 0u);
+}
+
+// The observation (E, planes, N, N) of nb <= BPW consecutive boards whose words
+// the wave holds -- board kb's black / white / possible_moves words and its
+// obs_flags in lane kb * LS (LS lanes per board) -- streamed into their
+// contiguous output region `base` (nb x planes x N*N/4 quads), one 64-quad
+// vector store per step, each lane taking the words of the board its quad
+// belongs to from that board's lane (ds_bpermute).  Every lane of the wave
+// must take part (ds_bpermute reads an inactive source lane as 0).  Used by
+// k_observe_w (the boards loaded from HBM) and by the step kernels' fused
+// observation (oth_step_observe / oth_sample_step_observe: the boards as the
+// step left them in registers).
+template <int N, int LAYOUT, typename T, int BPW, int LS = 1>
+__device__ __forceinline__ void obs_stream(const uint64_t (&bw)[Geo<N>::W], const uint64_t (&ww)[Geo<N>::W],
+                                           const uint64_t (&lw)[Geo<N>::W], uint32_t fl, int nb,
+                                           T* __restrict__ base) {
+    static_assert(BPW * LS <= 64, "the wave holds its boards");
     constexpr int W = Geo<N>::W;
     constexpr int NN = N * N;
     static_assert(NN % 4 == 0, "quads of squares");
     constexpr int Q = NN / 4;
-    constexpr int PLANES = LAYOUT == OTH_OBS_BOARD_LEGAL ? 2 : (LAYOUT == OTH_OBS_MAKE_STATE ? 4 : 1);
-    constexpr int PQ = PLANES * Q;  // quads per board
-    constexpr bool NEED_L = LAYOUT == OTH_OBS_BOARD_LEGAL || LAYOUT == OTH_OBS_MAKE_STATE || LAYOUT == OTH_OBS_LEGAL;
+    constexpr int PQ = obs_planes<LAYOUT>() * Q;  // quads per board
+    constexpr bool NEED_L = obs_needs_legal<LAYOUT>();
     const int lane = threadIdx.x & 63;
-    const long long e0 = ((long long)blockIdx.x * BLOCK + threadIdx.x - lane) / 64 * BPW;  // the wave's first board
-    if (e0 >= E) return;                                                                 // wave-uniform
-    const long long e = lane < BPW ? e0 + lane : E;  // lanes past BPW load nothing
-    uint64_t bw[W], ww[W], lw[W];
-    uint32_t fl = 0;  // bit 0: white to move; bit 1: more than one legal move (util.py:55)
-#pragma unroll
-    for (int k = 0; k < W; ++k) bw[k] = ww[k] = lw[k] = 0;
-    if (e < E) {
-        int cnt = 0;
-#pragma unroll
-        for (int k = 0; k < W; ++k) {
-            bw[k] = boards[(size_t)e * 2 * W + k];
-            ww[k] = boards[(size_t)e * 2 * W + W + k];
-            if constexpr (NEED_L) {
-                lw[k] = legal[(size_t)e * W + k];
-                cnt += popc64(lw[k]);
-            }
-        }
-        fl = ((meta[e] & M_TURN_WHITE) ? 1u : 0u) | (cnt > 1 ? 2u : 0u);
-    }
-    const int nb = (int)(E - e0 < BPW ? E - e0 : BPW);
     const int total = nb * PQ;
-    T* base = out + (size_t)e0 * PQ * 4;
     auto fetch = [&](const uint64_t (&x)[W], int kb, int wi) __attribute__((always_inline)) {
         uint64_t r = 0;
 #pragma unroll
         for (int k = 0; k < W; ++k) {
-            const uint64_t y = (uint64_t)__shfl((unsigned long long)x[k], kb);
+            const uint64_t y = (uint64_t)__shfl((unsigned long long)x[k], kb * LS);
             r = wi == k ? y : r;
         }
         return r;
@@ -1867,7 +1861,7 @@ __global__ __launch_bounds__(BLOCK) void k_observe_w(const uint64_t* __restrict_
         const uint32_t plane = rr / Q, q = rr - plane * Q;
         const uint32_t a0 = 4 * q, wi = a0 / 64, bi = a0 % 64;  // 4 | 64: a quad never straddles words
         const uint64_t xb = fetch(bw, (int)kb, (int)wi), xw = fetch(ww, (int)kb, (int)wi);
-        const uint32_t flk = (uint32_t)__shfl((int)fl, (int)kb);
+        const uint32_t flk = (uint32_t)__shfl((int)fl, (int)kb * LS);
         const bool tw = (flk & 1u) != 0;
         uint64_t xl = 0;
         if constexpr (NEED_L) xl = fetch(lw, (int)kb, (int)wi);
@@ -1904,6 +1898,150 @@ __global__ __launch_bounds__(BLOCK) void k_observe_w(const uint64_t* __restrict_
             }
         }
         if (g0 + lane < total) put_quad<T>(base, (uint32_t)g, v[0], v[1], v[2], v[3]);
+    }
+}
+
+// k_observe_w: the same values as k_observe, one wave per BPW consecutive
+// boards.  Each lane loads one board (coalesced), then the wave streams the
+// boards' output region (obs_stream).  One board per wave (round 2's
+// k_observe_q, each wave waiting on its own board's loads before one 1-KiB
+// store) reached 2.6 TB/s for make_state f32 at 1,048,576 boards; one wave's
+// loads feeding 64 boards' stores, 5.0 (a plain fill: 6.9).  BPW boards per wave
+// (64, or 16 for small launches: four times the waves, each streaming a quarter
+// of the region, so the store streams start sooner and more of them are in
+// flight).
+template <int N, int LAYOUT, typename T, int BPW = 64>
+__global__ __launch_bounds__(BLOCK) void k_observe_w(const uint64_t* __restrict__ boards,
+                                                     const uint16_t* __restrict__ meta,
+                                                     const uint64_t* __restrict__ legal, int E, T* __restrict__ out) {
+    static_assert(BPW == 4 || BPW == 8 || BPW == 16 || BPW == 32 || BPW == 64, "boards per wave");
+    constexpr int W = Geo<N>::W;
+    constexpr int PQ = obs_planes<LAYOUT>() * N * N / 4;  // quads per board
+    const int lane = threadIdx.x & 63;
+    const long long e0 = ((long long)blockIdx.x * BLOCK + threadIdx.x - lane) / 64 * BPW;  // the wave's first board
+    if (e0 >= E) return;                                                                 // wave-uniform
+    const long long e = lane < BPW ? e0 + lane : E;  // lanes past BPW load nothing
+    uint64_t bw[W], ww[W], lw[W];
+    uint32_t fl = 0;
+#pragma unroll
+    for (int k = 0; k < W; ++k) bw[k] = ww[k] = lw[k] = 0;
+    if (e < E) {
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+            bw[k] = boards[(size_t)e * 2 * W + k];
+            ww[k] = boards[(size_t)e * 2 * W + W + k];
+            if constexpr (obs_needs_legal<LAYOUT>()) lw[k] = legal[(size_t)e * W + k];
+        }
+        fl = obs_flags<W>(meta[e], lw);
+    }
+    const int nb = (int)(E - e0 < BPW ? E - e0 : BPW);
+    obs_stream<N, LAYOUT, T, BPW, 1>(bw, ww, lw, fl, nb, out + (size_t)e0 * PQ * 4);
+}
+
+// The fused observation of the step kernels (oth_step_observe,
+// oth_sample_step_observe): obs_stream for a runtime layout and dtype (kernel
+// arguments, so the switch is a scalar branch taken once per wave), into the
+// region of the wave's first board e0.  layout < 0: no observation.  Only
+// N*N % 4 == 0 (the quad stores); the C ABI takes two launches for other N.
+template <int N, int BPW, int LS>
+__device__ __forceinline__ void obs_tail(int layout, int dtype, void* __restrict__ out, long long e0,
+                                         const uint64_t (&bw)[Geo<N>::W], const uint64_t (&ww)[Geo<N>::W],
+                                         const uint64_t (&lw)[Geo<N>::W], uint32_t m, int nb) {
+    if constexpr ((N * N) % 4 == 0) {
+        if (layout < 0 || nb <= 0) return;
+        const uint32_t fl = obs_flags<Geo<N>::W>(m, lw);
+        auto by_type = [&](auto LC) __attribute__((always_inline)) {
+            constexpr int LAY = decltype(LC)::value;
+            constexpr size_t PER = (size_t)obs_planes<LAY>() * N * N;  // elements per board
+            switch (dtype) {
+                case OTH_I8:
+                    obs_stream<N, LAY, int8_t, BPW, LS>(bw, ww, lw, fl, nb, (int8_t*)out + e0 * PER);
+                    break;
+                case OTH_I32:
+                    obs_stream<N, LAY, int32_t, BPW, LS>(bw, ww, lw, fl, nb, (int32_t*)out + e0 * PER);
+                    break;
+                case OTH_I64:
+                    obs_stream<N, LAY, long long, BPW, LS>(bw, ww, lw, fl, nb, (long long*)out + e0 * PER);
+                    break;
+                case OTH_F32:
+                    obs_stream<N, LAY, float, BPW, LS>(bw, ww, lw, fl, nb, (float*)out + e0 * PER);
+                    break;
+                default:
+                    obs_stream<N, LAY, double, BPW, LS>(bw, ww, lw, fl, nb, (double*)out + e0 * PER);
+                    break;
+            }
+        };
+        switch (layout) {
+            case OTH_OBS_BOARD: by_type(std::integral_constant<int, OTH_OBS_BOARD>{}); break;
+            case OTH_OBS_BOARD_LEGAL: by_type(std::integral_constant<int, OTH_OBS_BOARD_LEGAL>{}); break;
+            case OTH_OBS_MAKE_STATE: by_type(std::integral_constant<int, OTH_OBS_MAKE_STATE>{}); break;
+            case OTH_OBS_ABSOLUTE: by_type(std::integral_constant<int, OTH_OBS_ABSOLUTE>{}); break;
+            default: by_type(std::integral_constant<int, OTH_OBS_LEGAL>{}); break;
+        }
+    }
+}
+
+// oth_step_sync: one board -- the single-board drop-in classes (BASELINE config
+// 1) -- stepped with a host action passed by value, then its whole record
+// (oth_record: state, reward / done, count_disks, GreedyPolicy's move,
+// get_observation and board_state) written into mapped host memory by the same
+// launch, the sequence number last behind a system-scope fence, so the host
+// can read the record as soon as that number lands.  One wave: every lane
+// holds the board (the step is tiny), lane 0 stores the state back, the lanes
+// write the squares of the observation planes.
+template <int N>
+__global__ __launch_bounds__(64) void k_record(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
+                                               uint64_t* __restrict__ legal, int board, int step, int action,
+                                               uint32_t flags, int planes, unsigned long long* __restrict__ wdl,
+                                               Rng rng, uint64_t ply, oth_record* __restrict__ rec, uint32_t seq) {
+    constexpr int W = Geo<N>::W, NN = N * N;
+    static_assert(W <= OTH_RECORD_MAX_WORDS && NN <= OTH_RECORD_MAX_SQUARES, "record capacity");
+    ply += *rng.ply_off;
+    const int lane = threadIdx.x;
+    WaveSlot slot(wdl, board >> 6);
+    Lane<N> s;
+    load_lane<N>(s, boards, meta, legal, board);
+    int r = 0, d = 0, win = NO_DISK;
+    bool ended = false;
+    if (step) {
+        const bool was_term = (s.meta & M_TERMINATED) != 0;
+        step_lane<N>(s, action, flags, r, d, win, Solo<N>(0, nullptr));
+        ended = d && !was_term;
+        if (ended && (flags & OTH_AUTO_RESET))
+            reset_lane<N>(s, rng.seed, rng.id_base + (uint32_t)board, ply, RNG_OPENING_AUTO, rng.init_rand);
+        if (lane == 0 && !was_term) store_lane<N>(s, boards, meta, legal, board);
+    }
+    slot.count(lane == 0 && ended && win == BLACK_DISK, lane == 0 && ended && win == NO_DISK,
+               lane == 0 && ended && win == WHITE_DISK);
+    slot.flush();
+    const bool tw = (s.meta & M_TURN_WHITE) != 0;
+    const int sign = tw ? 1 : -1;  // othello.py:364-369: mover +1
+    for (int a = lane; a < NN; a += 64) {
+        const int isb = (int)((s.black.w[a / 64] >> (a % 64)) & 1u), isw = (int)((s.white.w[a / 64] >> (a % 64)) & 1u);
+        rec->board_state[a] = (int8_t)(isw - isb);
+        rec->obs[a] = (int8_t)((isw - isb) * sign);
+        if (planes == 2) rec->obs[NN + a] = (int8_t)((s.legal.w[a / 64] >> (a % 64)) & 1u);
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+            rec->black[i] = s.black.w[i];
+            rec->white[i] = s.white.w[i];
+            rec->legal[i] = s.legal.w[i];
+        }
+        rec->meta = (uint16_t)s.meta;
+        rec->done = (uint8_t)d;
+        rec->planes = (uint8_t)planes;
+        rec->reward = r;
+        rec->white_cnt = popcount(s.white);
+        rec->black_cnt = popcount(s.black);
+        rec->greedy = popcount(s.legal) ? greedy_action<N>(s, Solo<N>(0, nullptr)) : -1;
+    }
+    __threadfence_system();  // every lane's record bytes before the sequence number
+    __syncthreads();
+    if (lane == 0) {
+        __threadfence_system();
+        *reinterpret_cast<volatile uint32_t*>(&rec->seq) = seq;
     }
 }
 

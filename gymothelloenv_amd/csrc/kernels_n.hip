@@ -42,6 +42,19 @@ int with_policy(int policy, Fn&& fn) {
     }
 }
 
+// the step kernels' fused observation (obs_tail): none, or a layout / dtype / output
+struct ObsOut {
+    int layout = -1;
+    int dtype = 0;
+    void* out = nullptr;
+};
+// obs_tail's quad stores need N*N % 4 == 0 and an output aligned to 4 elements
+template <int N>
+bool obs_fusable(int dtype, const void* out) {
+    static const int esize[5] = {1, 4, 8, 4, 8};
+    return (N * N) % 4 == 0 && dtype >= OTH_I8 && dtype <= OTH_F64 && (uintptr_t)out % (4 * esize[dtype]) == 0;
+}
+
 }  // namespace
 
 template <int N>
@@ -78,6 +91,27 @@ int launch_step(oth_env* env, const int32_t* actions, int32_t* rewards, uint8_t*
     launch_k(k_step<N>, dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards, env->meta, env->legal,
              env->E, env->flags, actions, rewards, dones, env->wdl, rng_of(env), ply);
     return after_launch("oth_step");
+}
+
+// oth_step_observe: one-word boards step and observe in one launch (k_ply_step_obs,
+// ply.hpp); other sizes, or an output the quad stores cannot write, take
+// oth_step's kernel and then oth_observe's
+template <int N>
+int launch_step_observe(oth_env* env, const int32_t* actions, int32_t* rewards, uint8_t* dones, int layout, int dtype,
+                        void* obs, uint64_t ply, hipStream_t st) {
+    if constexpr (Geo<N>::W == 1 && (N * N) % 4 == 0) {
+        if (obs_fusable<N>(dtype, obs)) {
+            constexpr int BPW = OTH_SO_BPW;
+            const long long waves = ((long long)env->E + BPW - 1) / BPW;
+            launch_k((k_ply_step_obs<N, OTH_SO_LPB, BPW>), dim3(grid_for(waves * 64)), dim3(BLOCK), 0, st,
+                     env->boards, env->meta, env->legal, env->E, env->flags, actions, rewards, dones, env->wdl,
+                     rng_of(env), ply, layout, dtype, obs);
+            return after_launch("oth_step_observe");
+        }
+    }
+    const int rc = launch_step<N>(env, actions, rewards, dones, ply, st);
+    if (rc) return rc;
+    return launch_observe<N>(env, layout, dtype, obs, st);
 }
 
 // k_play with the REC specialisation where all per-ply outputs are stored
@@ -154,7 +188,7 @@ int launch_play(oth_env* env, int policy, int n_plies, int32_t* actions, int32_t
 template <int N, int G, bool VEC, bool FULL>
 void launch_ss(oth_env* env, const float* logits, long long ld, const float* uniforms, uint64_t counter, int mode,
                int32_t* actions, float* log_probs, float* entropy, int32_t* rewards, uint8_t* dones, uint64_t ply,
-               hipStream_t st) {
+               const ObsOut& ob, hipStream_t st) {
     // lane quads (k_sample_step4) while the quads fill at most one wave per SIMD: latency-bound sizes,
     // where a quarter of the per-lane instruction stream wins (8x8, E = 3001: 5.67 -> 4.83 us per ply);
     // beyond, the quads' duplicated step work loses to pairs (65,536: 7.02 -> 7.45)
@@ -163,7 +197,8 @@ void launch_ss(oth_env* env, const float* logits, long long ld, const float* uni
         if (env->E <= OTH_SS_QUAD_MAX_E && grid_for(4LL * env->E) <= env->nslots) {
             launch_k((k_sample_step4<N, VEC, FULL>), dim3(grid_for(4LL * env->E)), dim3(BLOCK), 0, st,
                      env->boards, env->meta, env->legal, env->E, env->flags, logits, ld, uniforms, counter,
-                     mode, actions, log_probs, entropy, rewards, dones, env->wdl, rng_of(env), ply);
+                     mode, actions, log_probs, entropy, rewards, dones, env->wdl, rng_of(env), ply, ob.layout, ob.dtype,
+                     ob.out);
             return;
         }
     }
@@ -178,7 +213,8 @@ void launch_ss(oth_env* env, const float* logits, long long ld, const float* uni
         if (PAIR1 || VEC || env->E <= OTH_SS_PAIR_W_MAX_E) {
             launch_k((k_sample_step2<N, VEC, FULL>), dim3(grid_for(2LL * env->E)), dim3(BLOCK), 0, st,
                      env->boards, env->meta, env->legal, env->E, env->flags, logits, ld, uniforms, counter,
-                     mode, actions, log_probs, entropy, rewards, dones, env->wdl, rng_of(env), ply);
+                     mode, actions, log_probs, entropy, rewards, dones, env->wdl, rng_of(env), ply, ob.layout, ob.dtype,
+                     ob.out);
             return;
         }
     }
@@ -187,7 +223,7 @@ void launch_ss(oth_env* env, const float* logits, long long ld, const float* uni
     const long long lanes = ONE ? (long long)env->E : ((long long)env->E + G - 1) / G * G;
     launch_k((k_sample_step<N, G, VEC, FULL, ONE>), dim3(grid_for(lanes)), dim3(BLOCK), 0, st, env->boards,
              env->meta, env->legal, env->E, env->flags, logits, ld, uniforms, counter, mode, actions,
-             log_probs, entropy, rewards, dones, env->wdl, rng_of(env), ply);
+             log_probs, entropy, rewards, dones, env->wdl, rng_of(env), ply, ob.layout, ob.dtype, ob.out);
 }
 
 // the sampler's lanes per board: k_masked's choice for the board's word count
@@ -195,23 +231,29 @@ void launch_ss(oth_env* env, const float* logits, long long ld, const float* uni
 template <int N>
 int launch_sample_step(oth_env* env, const float* logits, long long ld, const float* uniforms, uint64_t counter,
                        int mode, int32_t* actions, float* log_probs, float* entropy, int32_t* rewards, uint8_t* dones,
-                       uint64_t ply, hipStream_t st) {
+                       uint64_t ply, int obs_layout, int obs_dtype, void* obs, hipStream_t st) {
     constexpr int G = Geo<N>::W <= 2 ? oth_ms::MS_G : 16;
     const bool vec = ((N * N) % 4 == 0) && (ld % 4 == 0) && (((uintptr_t)logits & 15u) == 0);
     const bool full = (mode & OTH_MASKED_FULL_ENTROPY) != 0;
     const int base = mode & 3;
+    // the observation from the step kernel's registers where its quad stores can
+    // write `obs`; else a k_observe launch after it (the same values)
+    const bool fuse = obs && obs_fusable<N>(obs_dtype, obs);
+    const ObsOut ob = fuse ? ObsOut{obs_layout, obs_dtype, obs} : ObsOut{};
     if (vec) {
         if (full) launch_ss<N, G, true, true>(env, logits, ld, uniforms, counter, base, actions, log_probs, entropy,
-                                              rewards, dones, ply, st);
+                                              rewards, dones, ply, ob, st);
         else launch_ss<N, G, true, false>(env, logits, ld, uniforms, counter, base, actions, log_probs, entropy,
-                                          rewards, dones, ply, st);
+                                          rewards, dones, ply, ob, st);
     } else {
         if (full) launch_ss<N, G, false, true>(env, logits, ld, uniforms, counter, base, actions, log_probs,
-                                               entropy, rewards, dones, ply, st);
+                                               entropy, rewards, dones, ply, ob, st);
         else launch_ss<N, G, false, false>(env, logits, ld, uniforms, counter, base, actions, log_probs, entropy,
-                                           rewards, dones, ply, st);
+                                           rewards, dones, ply, ob, st);
     }
-    return after_launch("oth_sample_step");
+    const int rc = after_launch("oth_sample_step");
+    if (rc || !obs || fuse) return rc;
+    return launch_observe<N>(env, obs_layout, obs_dtype, obs, st);
 }
 
 template <int N>
@@ -328,6 +370,14 @@ int launch_observe(oth_env* env, int layout, int dtype, void* out, hipStream_t s
     return after_launch("oth_observe");
 }
 
+// oth_step_sync: one wave steps / records one board into the mapped host record
+template <int N>
+int launch_record(oth_env* env, int board, int step, int action, int planes, uint64_t ply, hipStream_t st) {
+    launch_k(k_record<N>, dim3(1), dim3(64), 0, st, env->boards, env->meta, env->legal, board, step, action,
+             env->flags, planes, env->wdl, rng_of(env), ply, env->rec_dev, env->rec_seq);
+    return after_launch("oth_step_sync");
+}
+
 template <int N>
 int launch_set_turn(oth_env* env, int turn, const uint8_t* mask, hipStream_t st) {
     launch_k(k_set_turn<N>, dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards, env->meta, env->legal,
@@ -348,12 +398,15 @@ template int launch_reset_vs<OTH_N>(oth_env*, int, const int8_t*, const uint8_t*
 template int launch_step_vs<OTH_N>(oth_env*, int, const int32_t*, const int8_t*, int32_t*, uint8_t*, int32_t*,
                                    uint64_t, hipStream_t);
 template int launch_sample_step<OTH_N>(oth_env*, const float*, long long, const float*, uint64_t, int, int32_t*,
-                                       float*, float*, int32_t*, uint8_t*, uint64_t, hipStream_t);
+                                       float*, float*, int32_t*, uint8_t*, uint64_t, int, int, void*, hipStream_t);
+template int launch_step_observe<OTH_N>(oth_env*, const int32_t*, int32_t*, uint8_t*, int, int, void*, uint64_t,
+                                        hipStream_t);
 template int launch_policy_actions<OTH_N>(oth_env*, int, int32_t*, hipStream_t);
 template int launch_legal_moves<OTH_N>(int, const uint64_t*, const uint64_t*, uint64_t*, hipStream_t);
 template int launch_observe<OTH_N>(oth_env*, int, int, void*, hipStream_t);
 template int launch_set_turn<OTH_N>(oth_env*, int, const uint8_t*, hipStream_t);
 template int launch_count<OTH_N>(oth_env*, int32_t*, hipStream_t);
 template int launch_fill_rays<OTH_N>(oth_env*, hipStream_t);
+template int launch_record<OTH_N>(oth_env*, int, int, int, int, uint64_t, hipStream_t);
 
 }  // namespace oth_host

@@ -41,6 +41,9 @@ struct oth_env {
     uint64_t ply_saved;       // eager ply counter while a region is open
     uint64_t* rays;           // one-word boards: the 8 x 64 ray table (fill_rays<N, true>) then the 256-word
                               // sel8 table (TABLE_WORDS), read by the single-ply kernels and k_play_rand
+    oth_record* rec_host;     // oth_step_sync's record: mapped pinned host memory (allocated on first use)
+    oth_record* rec_dev;      // its device address
+    uint32_t rec_seq;         // the last record's sequence number
 };
 
 namespace oth_host {
@@ -86,9 +89,13 @@ template <int N>
 int launch_step_vs(oth_env* env, int policy, const int32_t* actions, const int8_t* prot, int32_t* rewards,
                    uint8_t* dones, int32_t* plies, uint64_t call, hipStream_t st);
 template <int N>
+int launch_step_observe(oth_env* env, const int32_t* actions, int32_t* rewards, uint8_t* dones, int layout, int dtype,
+                        void* obs, uint64_t ply, hipStream_t st);
+// obs: NULL, or the observation (layout, dtype) of the boards after the step (oth_sample_step_observe)
+template <int N>
 int launch_sample_step(oth_env* env, const float* logits, long long ld, const float* uniforms, uint64_t counter,
                        int mode, int32_t* actions, float* log_probs, float* entropy, int32_t* rewards, uint8_t* dones,
-                       uint64_t ply, hipStream_t st);
+                       uint64_t ply, int obs_layout, int obs_dtype, void* obs, hipStream_t st);
 template <int N> int launch_policy_actions(oth_env* env, int policy, int32_t* out, hipStream_t st);
 template <int N>
 int launch_legal_moves(int n, const uint64_t* mover, const uint64_t* opp, uint64_t* out, hipStream_t st);
@@ -96,6 +103,8 @@ template <int N> int launch_observe(oth_env* env, int layout, int dtype, void* o
 template <int N> int launch_set_turn(oth_env* env, int turn, const uint8_t* mask, hipStream_t st);
 template <int N> int launch_count(oth_env* env, int32_t* out, hipStream_t st);
 template <int N> int launch_fill_rays(oth_env* env, hipStream_t st);
+template <int N>
+int launch_record(oth_env* env, int board, int step, int action, int planes, uint64_t ply, hipStream_t st);
 // k_play_rand (one-word boards, random and greedy) and k_play_rand_w (two-word boards,
 // random) in play_rand_n.hip, N = 4..11, with its own scheduler flags
 template <int N, int POL>

@@ -346,6 +346,92 @@ __global__ __launch_bounds__(BLOCK) void k_ply_step(uint64_t* __restrict__ board
                                    rays, rng, ply);
 }
 
+// oth_step_observe on one-word boards: OthelloBaseEnv.step (othello.py:412-462)
+// with the caller's actions and the returned get_observation() (:462) -- or any
+// oth_observe layout and dtype -- in one launch: the wave steps its BPW boards
+// (LPB lanes per board: one lane with computed rays, or a lane pair splitting
+// the flips and the scans as k_sample_step2), stores the state, then streams
+// the boards' observations from registers (obs_tail: the state as the step --
+// and an auto-reset -- left it, exactly what oth_observe after oth_step reads,
+// without reading it back).  BPW < 64 / LPB leaves lanes idle during the step
+// (they step a copy of the wave's last board and store nothing) and gives the
+// store stream more waves per SIMD: at 65,536 boards the observation's store
+// loop wants four waves per SIMD (k_observe_w's 16 boards per wave), the step
+// one (k_ply_step).
+#ifndef OTH_SO_LPB
+#define OTH_SO_LPB 1  // lanes per board of k_ply_step_obs
+#endif
+#ifndef OTH_SO_BPW
+#define OTH_SO_BPW 16  // boards per wave of k_ply_step_obs
+#endif
+template <int N, int LPB, int BPW>
+__global__ __launch_bounds__(BLOCK) void k_ply_step_obs(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,
+                                                        uint64_t* __restrict__ legal, int E, uint32_t flags,
+                                                        const int32_t* __restrict__ actions,
+                                                        int32_t* __restrict__ rewards, uint8_t* __restrict__ dones,
+                                                        unsigned long long* __restrict__ wdl, Rng rng, uint64_t ply,
+                                                        int layout, int dtype, void* __restrict__ obs) {
+    static_assert(Geo<N>::W == 1, "one-word boards");
+    static_assert((LPB == 1 || LPB == 2) && LPB * BPW <= 64 && BPW >= 16, "lanes per board, boards per wave");
+    constexpr int NN = N * N;
+    constexpr int RAYS = LPB == 2 ? RAYS_PAIR : RAYS_MATH;
+    ply += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
+    const int lane = threadIdx.x & 63;
+    const int wave = (int)(((long long)blockIdx.x * BLOCK + threadIdx.x) >> 6);
+    const long long e0 = (long long)wave * BPW;
+    if (e0 >= E) return;  // wave-uniform
+    const int nb = (int)(E - e0 < BPW ? E - e0 : BPW);
+    const int kb = lane / LPB, h = lane % LPB;
+    const bool mine = kb < nb;                                 // lanes past the wave's boards (or past
+    const int e = (int)e0 + (mine ? kb : nb - 1);              // BPW) step a copy of its last one
+    const ulonglong2 bw = reinterpret_cast<const ulonglong2*>(boards)[e];
+    uint64_t L = legal[e];
+    uint32_t m = meta[e];
+    const int a = actions[e];
+    WaveSlot slot(wdl, wave);  // (ceil(E / BPW) <= the handle's ceil(4E / 64) slots for BPW >= 16)
+    const uint32_t id = rng.id_base + (uint32_t)e;
+    uint64_t B = bw.x, Wt = bw.y;
+    const bool was_term = (m & M_TERMINATED) != 0;
+    const bool valid = (unsigned)a < (unsigned)NN && ((L >> (a & 63)) & 1ull);  // (:417)
+    int r, d, win;
+    const uint64_t L0 = L;
+    const uint32_t m0 = m;
+    step1<N, RAYS>(B, Wt, L, m, a, valid, flags, nullptr, r, d, win, h);
+    if (was_term) {  // a no-op reporting done (othello.py:415-416): the state stays as it was
+        r = 0;
+        d = 1;
+        B = bw.x;
+        Wt = bw.y;
+        L = L0;
+        m = m0;
+    }
+    const bool ended = mine && d && !was_term;
+    if (ended && (flags & OTH_AUTO_RESET)) {  // reset (othello.py:256-271), black to move
+        B = Start<N>::BLACK.w[0];
+        Wt = Start<N>::WHITE.w[0];
+        constexpr uint64_t START_MOVES = start_moves<N>();
+        L = START_MOVES;
+        uint32_t rl = 0;
+        if (rng.init_rand > 0)
+            rl = (uint32_t)scale_index(philox_x(rng.seed, id, ply, RNG_OPENING_AUTO), rng.init_rand / 2 + 1) * 2u;
+        m = (rl & 0xffu) << M_RAND_SHIFT;
+    }
+    if (mine && h == 0) {
+        if (!was_term) {
+            reinterpret_cast<ulonglong2*>(boards)[e] = ulonglong2{B, Wt};
+            legal[e] = L;
+            meta[e] = (uint16_t)m;
+        }
+        if (rewards) rewards[e] = r;
+        if (dones) dones[e] = (uint8_t)d;
+    }
+    const bool h0 = h == 0;
+    slot.count(h0 && ended && win == BLACK_DISK, h0 && ended && win == NO_DISK, h0 && ended && win == WHITE_DISK);
+    slot.flush();
+    const uint64_t ob[1] = {B}, ow[1] = {Wt}, ol[1] = {L};
+    obs_tail<N, BPW, LPB>(layout, dtype, obs, e0, ob, ow, ol, m, nb);
+}
+
 // oth_step_policy(RANDOM, 1 ply) on one-word boards
 template <int N, int RAYS>
 __global__ __launch_bounds__(BLOCK) void k_ply_rand(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,

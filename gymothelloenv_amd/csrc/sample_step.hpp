@@ -28,7 +28,8 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step(uint64_t* __restrict__ bo
                                                        int32_t* __restrict__ actions, float* __restrict__ log_probs,
                                                        float* __restrict__ entropy, int32_t* __restrict__ rewards,
                                                        uint8_t* __restrict__ dones,
-                                                       unsigned long long* __restrict__ wdl, Rng rng, uint64_t ply) {
+                                                       unsigned long long* __restrict__ wdl, Rng rng, uint64_t ply,
+                                                       int obs_layout, int obs_dtype, void* __restrict__ obs) {
     constexpr int NN = N * N;
     constexpr int CH = Geo<N>::W;
     ply += rng.ply_off[0];      // graph-region offsets (oth_graph_end); 0 eagerly
@@ -91,6 +92,10 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step(uint64_t* __restrict__ bo
     }
     slot.count(cb != 0, cd != 0, cw != 0);
     slot.flush();
+    // oth_sample_step_observe: the wave's 64 boards' observations (lane = board)
+    const long long e0 = t - (threadIdx.x & 63);
+    obs_tail<N, 64, 1>(obs_layout, obs_dtype, obs, e0, s.black.w, s.white.w, s.legal.w, s.meta,
+                       (int)(E - e0 < 64 ? E - e0 : 64));
 }
 
 // k_sample_step on lane pairs (boards of one or two words): the pair samples
@@ -111,7 +116,8 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step2(uint64_t* __restrict__ b
                                                         int mode, int32_t* __restrict__ actions,
                                                         float* __restrict__ log_probs, float* __restrict__ entropy,
                                                         int32_t* __restrict__ rewards, uint8_t* __restrict__ dones,
-                                                        unsigned long long* __restrict__ wdl, Rng rng, uint64_t ply) {
+                                                        unsigned long long* __restrict__ wdl, Rng rng, uint64_t ply,
+                                                        int obs_layout, int obs_dtype, void* __restrict__ obs) {
     constexpr int W = Geo<N>::W;
     static_assert(W <= 2 && oth_ms::MS_G == 4, "lane pairs restate k_masked's four lanes of boards of <= 2 words");
     constexpr int NN = N * N;
@@ -182,6 +188,11 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step2(uint64_t* __restrict__ b
     }
     slot.count(cb != 0, cd != 0, cw != 0);  // (h == 0 lanes only)
     slot.flush();
+    // oth_sample_step_observe: the wave's 32 boards' observations (both lanes of a
+    // pair hold the board as stepped and reset)
+    const long long e0 = (gt - (threadIdx.x & 63)) >> 1;
+    obs_tail<N, 32, 2>(obs_layout, obs_dtype, obs, e0, s.black.w, s.white.w, s.legal.w, s.meta,
+                       (int)(E - e0 < 32 ? E - e0 : 32));
 }
 
 // k_sample_step on lane quads (one-word boards): the quad IS k_masked's group
@@ -197,7 +208,8 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step4(uint64_t* __restrict__ b
                                                         int mode, int32_t* __restrict__ actions,
                                                         float* __restrict__ log_probs, float* __restrict__ entropy,
                                                         int32_t* __restrict__ rewards, uint8_t* __restrict__ dones,
-                                                        unsigned long long* __restrict__ wdl, Rng rng, uint64_t ply) {
+                                                        unsigned long long* __restrict__ wdl, Rng rng, uint64_t ply,
+                                                        int obs_layout, int obs_dtype, void* __restrict__ obs) {
     static_assert(Geo<N>::W == 1 && oth_ms::MS_G == 4, "lane quads are k_masked's four lanes of one-word boards");
     constexpr int NN = N * N;
     ply += rng.ply_off[0];      // graph-region offsets (oth_graph_end); 0 eagerly
@@ -244,6 +256,11 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step4(uint64_t* __restrict__ b
     }
     slot.count(cb != 0, cd != 0, cw != 0);  // (q == 0 lanes only)
     slot.flush();
+    // oth_sample_step_observe: the wave's 16 boards' observations (the quad's four
+    // lanes hold the board as stepped and reset)
+    const long long e0 = (gt - (threadIdx.x & 63)) >> 2;
+    obs_tail<N, 16, 4>(obs_layout, obs_dtype, obs, e0, s.black.w, s.white.w, s.legal.w, s.meta,
+                       (int)(E - e0 < 16 ? E - e0 : 16));
 }
 
 }  // namespace oth_dev

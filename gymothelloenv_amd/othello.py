@@ -11,6 +11,8 @@ The wrappers (SimpleOthelloEnv, OthelloEnv) are the reference's host-side
 control flow around that engine, with the same np.random.RandomState calls
 in the same order, so seeded runs reproduce the reference's trajectories.
 """
+import ctypes
+
 import numpy as np
 import torch
 
@@ -72,26 +74,15 @@ class OthelloBaseEnv(object):
         self._vec = VecOthelloEnv(1, board_size=n, sudden_death_on_invalid_move=sudden_death_on_invalid_move,
                                   num_disk_as_reward=num_disk_as_reward,
                                   possible_actions_in_obs=possible_actions_in_obs, device=device)
-        dev = self._vec.device
         self._planes = 2 if possible_actions_in_obs else 1
-        W, nn = self._W, n * n
-        # packed staging: boards | legal | meta | reward, done | counts | obs | board_state
-        self._o_boards, self._o_legal = 0, 16 * W
-        self._o_meta = 24 * W
-        self._o_rew = 24 * W + 8
-        self._o_done = 24 * W + 12
-        self._o_cnt = 24 * W + 16
-        self._o_obs = 24 * W + 24
-        self._o_abs = self._o_obs + 8 * nn * self._planes
-        size = self._o_abs + 8 * nn
-        self._stage = torch.zeros(size, dtype=torch.uint8, device=dev)
-        self._host = torch.zeros(size, dtype=torch.uint8).pin_memory()
-        self._act = torch.zeros(1, dtype=torch.int32, device=dev)
-        self._act_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+        self._layout = L.OTH_OBS_BOARD_LEGAL if possible_actions_in_obs else L.OTH_OBS_BOARD
+        self._obs_shape = (2, n, n) if possible_actions_in_obs else (n, n)
+        self._sync_fn = self._vec._lib.oth_step_sync
+        self._recp = ctypes.c_void_p()
+        self._rec = None  # L.OthRecord over the handle's mapped host record (oth_step_sync)
         self._dirty = True
-        self._reward = 0
         # Initialize internal states (othello.py:238-242): no possible moves until reset().
-        self._vec.set_state(legal=torch.zeros(W, dtype=torch.int64))
+        self._vec.set_state(legal=torch.zeros(self._W, dtype=torch.int64))
         self.action_space = Discrete(n ** 2)
         if possible_actions_in_obs:
             self.observation_space = Box(np.zeros([2, n, n]), np.ones([2, n, n]))
@@ -99,50 +90,90 @@ class OthelloBaseEnv(object):
             self.observation_space = Box(np.zeros([n, n]), np.ones([n, n]))
 
     # ------------------------------------------------------------ device sync
-    def _view(self, off, dtype, count):
-        return self._stage[off:off + count * torch.tensor([], dtype=dtype).element_size()].view(dtype)
+    def _call(self, step, action=0):
+        """oth_step_sync: (step and) record the board in one launch and one wait;
+        the record stays in the handle's mapped host buffer, decoded lazily."""
+        v = self._vec
+        rc = self._sync_fn(v._hv, 0, step, action, self._layout, ctypes.byref(self._recp), v._stream())
+        if rc:
+            L.check(rc, "oth_step_sync")
+        if self._rec is None or ctypes.addressof(self._rec) != self._recp.value:
+            rec = self._rec = L.OthRecord.from_address(self._recp.value)
+            nn = self._n * self._n
+            self._obs_i8 = np.ctypeslib.as_array(rec.obs)[:self._planes * nn]
+            self._abs_i8 = np.ctypeslib.as_array(rec.board_state)[:nn]
+            self._legal_u64 = np.ctypeslib.as_array(rec.legal)[:self._W]
+        self._dirty = False
+        self._moves = None  # decoded possible_moves / board_state of this record
+        self._bs = None
 
     def _pull(self):
-        """Enqueue state / counts / observations into the staging buffer, one D2H copy, sync."""
-        v, lib, s = self._vec, self._vec._lib, self._vec._stream()
-        W, n, nn = self._W, self._n, self._n * self._n
-        b = self._view(self._o_boards, torch.int64, 2 * W)
-        lg = self._view(self._o_legal, torch.int64, W)
-        m = self._view(self._o_meta, torch.int16, 1)
-        L.check(lib.oth_get_state(v._h, L.ctypes.c_void_p(b.data_ptr()), L.ctypes.c_void_p(m.data_ptr()),
-                                  L.ctypes.c_void_p(lg.data_ptr()), s), "oth_get_state")
-        c = self._view(self._o_cnt, torch.int32, 2)
-        L.check(lib.oth_count_disks(v._h, L.ctypes.c_void_p(c.data_ptr()), s), "oth_count_disks")
-        lay = L.OTH_OBS_BOARD_LEGAL if self.possible_actions_in_obs else L.OTH_OBS_BOARD
-        o = self._view(self._o_obs, torch.int64, self._planes * nn)
-        L.check(lib.oth_observe(v._h, lay, L.OTH_I64, L.ctypes.c_void_p(o.data_ptr()), s), "oth_observe")
-        a = self._view(self._o_abs, torch.int64, nn)
-        L.check(lib.oth_observe(v._h, L.OTH_OBS_ABSOLUTE, L.OTH_I64, L.ctypes.c_void_p(a.data_ptr()), s),
-                "oth_observe")
-        self._host.copy_(self._stage, non_blocking=True)
-        torch.cuda.current_stream(v.device).synchronize()
-        h = self._host.numpy()
-        self._boards = h[self._o_boards:self._o_boards + 16 * W].view(np.uint64).copy()
-        self._legal = h[self._o_legal:self._o_legal + 8 * W].view(np.uint64).copy()
-        meta = int(h[self._o_meta:self._o_meta + 2].view(np.uint16)[0])
-        self._reward_dev = int(h[self._o_rew:self._o_rew + 4].view(np.int32)[0])
-        self._done_dev = int(h[self._o_done])
-        cnt = h[self._o_cnt:self._o_cnt + 8].view(np.int32)
-        self._white_cnt, self._black_cnt = np.int64(cnt[0]), np.int64(cnt[1])
-        obs = h[self._o_obs:self._o_obs + 8 * nn * self._planes].view(np.int64).copy()
-        self._obs = obs.reshape((2, n, n) if self.possible_actions_in_obs else (n, n))
-        self._board_state = h[self._o_abs:self._o_abs + 8 * nn].view(np.int64).copy().reshape(n, n)
-        self._meta = meta
-        self._player_turn = WHITE_DISK if meta & 1 else BLACK_DISK
-        self._terminated = bool(meta & 2)
-        wc = (meta >> 2) & 3
-        self._winner = WHITE_DISK if wc == 1 else (BLACK_DISK if wc == 2 else NO_DISK)
-        self._possible_moves = _mask_to_list(self._legal, nn)
-        self._dirty = False
+        self._call(0)
 
     def _sync(self):
         if self._dirty:
-            self._pull()
+            self._call(0)
+
+    @property
+    def _meta(self):
+        self._sync()
+        return self._rec.meta
+
+    @property
+    def _player_turn(self):
+        return WHITE_DISK if self._meta & 1 else BLACK_DISK
+
+    @property
+    def _terminated(self):
+        return bool(self._meta & 2)
+
+    @property
+    def _winner(self):
+        wc = (self._meta >> 2) & 3
+        return WHITE_DISK if wc == 1 else (BLACK_DISK if wc == 2 else NO_DISK)
+
+    @property
+    def _legal(self):
+        self._sync()
+        return self._legal_u64.copy()
+
+    @property
+    def _possible_moves(self):
+        self._sync()
+        if self._moves is None:
+            self._moves = _mask_to_list(self._legal_u64, self._n * self._n)
+        return self._moves
+
+    @property
+    def _board_state(self):
+        self._sync()
+        if self._bs is None:
+            self._bs = self._abs_i8.astype(np.int64).reshape(self._n, self._n)
+        return self._bs
+
+    @property
+    def _obs(self):
+        self._sync()
+        return self._obs_i8.astype(np.int64).reshape(self._obs_shape)
+
+    @property
+    def _white_cnt(self):
+        self._sync()
+        return np.int64(self._rec.white_cnt)
+
+    @property
+    def _black_cnt(self):
+        self._sync()
+        return np.int64(self._rec.black_cnt)
+
+    @property
+    def _reward_dev(self):
+        return self._rec.reward
+
+    def _greedy_move(self):
+        """GreedyPolicy.get_action for the side to move, from the record (-1: no move)."""
+        self._sync()
+        return self._rec.greedy
 
     def _push_meta(self, meta):
         self._vec.set_state(meta=torch.tensor([meta], dtype=torch.int16))
@@ -208,12 +239,12 @@ class OthelloBaseEnv(object):
     def reset(self):
         """othello.py:265-271"""
         self._vec.reset()
-        self._pull()
+        self._call(0)
         return self.get_observation()
 
     def step(self, action):
-        """othello.py:412-462: returns (observation, reward, done, None)."""
-        self._sync()
+        """othello.py:412-462: returns (observation, reward, done, None).  One
+        launch steps the board and writes its record to host memory (oth_step_sync)."""
         if self._terminated:
             raise ValueError('Game has terminated!')
         try:
@@ -222,16 +253,15 @@ class OthelloBaseEnv(object):
             a = -1
         if not -2 ** 31 <= a < 2 ** 31:
             a = -1  # outside int32: not in possible_moves either way
-        invalid = a not in self._possible_moves  # only for determine_winner's messages
-        self._act_host[0] = a
-        self._act.copy_(self._act_host, non_blocking=True)
-        rew = self._view(self._o_rew, torch.int32, 1)
-        done = self._view(self._o_done, torch.uint8, 1)
-        self._vec.step(self._act, rewards=rew, dones=done, observe=False)
-        self._pull()
-        if self._terminated and not self.mute:
+        if not self.mute:  # determine_winner's messages need the move's validity
+            nn = self._n * self._n
+            invalid = not (0 <= a < nn and (int(self._legal_u64[a // 64]) >> (a % 64)) & 1)
+        self._call(1, a)
+        rec = self._rec
+        done = bool(rec.meta & 2)
+        if done and not self.mute:
             self._print_result(invalid and self.sudden_death_on_invalid_move)
-        return self.get_observation(), self._reward_dev, self._terminated, None
+        return self._obs_i8.astype(np.int64).reshape(self._obs_shape), rec.reward, done, None
 
     def _print_result(self, sudden):
         """determine_winner's messages (othello.py:440-441, 476-500); `mute` silences them."""

@@ -46,7 +46,10 @@ class RandomPolicy(object):
 
 
 class GreedyPolicy(object):
-    """simple_policies.py:57-95, the candidate scan done by the k_greedy kernel."""
+    """simple_policies.py:57-95: the move the device computed for the side to move
+    (the bit-plane flip counts of every square, lowest square on ties) -- read
+    from the board's record, which the launch of the last step / reset wrote
+    (oth_step_sync): no device call of its own."""
 
     def __init__(self):
         self.env = None
@@ -58,9 +61,7 @@ class GreedyPolicy(object):
         obs = np.asarray(obs)
         if obs.ndim == 3 and obs.shape[0] == 4:  # make_state obs: same turn check as undo_state
             assert int((self.env.player_turn + 1) / 2) == int(obs[2][0][0])
-        vec = self.env._vec
-        self.env._sync()
-        a = int(vec.policy_actions("greedy").cpu()[0])
+        a = self.env._greedy_move()
         if a < 0:
             raise ValueError('no possible moves')
         return a

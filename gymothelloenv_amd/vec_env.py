@@ -80,7 +80,10 @@ class VecOthelloEnv(object):
         self._hv = h.value  # the handle as an int: the per-step ctypes calls take it as is
         self._dev_index = self.device.index
         self._step_fn = self._lib.oth_step
+        self._step_obs_fn = self._lib.oth_step_observe
         self._bview = None  # (dones tensor, its bool view): step()'s view of caller-given dones, cached
+        self._okbufs = None  # (rewards, dones) tensors step() has checked
+        self._okobs = None  # (obs tensor, layout) step() / sample_step() have checked
         self._sample_calls = 0  # Philox counter of sample_actions
         self._region_resets = None  # resets inside an open graph region (None: no region)
 
@@ -142,14 +145,20 @@ class VecOthelloEnv(object):
         L.check(self._lib.oth_reset(self._h, _ptr(m), self._stream()), "oth_reset")
         return self.get_observation()
 
-    def step(self, actions, rewards=None, dones=None, observe=True):
+    def step(self, actions, rewards=None, dones=None, observe=True, obs=None, obs_layout=None,
+             obs_dtype=torch.int64):
         """OthelloBaseEnv.step (othello.py:412-462) on every board.
 
-        actions: int tensor (E,).  rewards / dones: optional int32 / uint8 (E,)
-        tensors on this device, written in place (the loop form: no allocation
-        per step).  Returns (obs, rewards int32 (E,), dones bool (E,), None) --
-        obs is None when observe=False.  The host path is one ctypes call: an
-        int32 contiguous action tensor on this device is passed as is."""
+        actions: int tensor (E,).  rewards / dones: optional int32 / uint8 (or
+        bool) (E,) tensors on this device, written in place (the loop form: no
+        allocation per step; checked once per tensor).  Returns (obs, rewards
+        int32 (E,), dones bool (E,), None).  With observe (the default) obs is the
+        step's get_observation() (othello.py:462) -- or `obs_layout` ('board',
+        'board_legal', 'make_state', 'absolute', 'legal') -- written by the same
+        launch that stepped the boards (oth_step_observe), into `obs` if given (its
+        dtype decides the element type) or a new `obs_dtype` tensor; None when
+        observe=False.  The host path is one ctypes call: an int32 contiguous
+        action tensor on this device is passed as is."""
         a = actions
         if a.dtype is not torch.int32 or not a.is_contiguous() or a.device != self.device:
             a = a.to(device=self.device, dtype=torch.int32).contiguous()
@@ -157,15 +166,62 @@ class VecOthelloEnv(object):
             raise ValueError("expected %d actions, got %d" % (self.num_envs, a.numel()))
         r = rewards if rewards is not None else self._i32(self.num_envs)
         d = dones if dones is not None else self._u8(self.num_envs)
+        ok = self._okbufs
+        if ok is None or ok[0] is not r or ok[1] is not d:  # caller-given buffers: checked once each
+            self._check_out(r, (torch.int32,), "rewards")
+            self._check_out(d, (torch.uint8, torch.bool), "dones")
+            self._okbufs = (r, d)
         st = _RAW_STREAM(self._dev_index) if _RAW_STREAM is not None else self._stream()
-        rc = self._step_fn(self._hv, a.data_ptr(), r.data_ptr(), d.data_ptr(), st)
-        if rc:
-            L.check(rc, "oth_step")
-        obs = self.get_observation() if observe else None
+        if observe:
+            lay, o = self._obs_out(obs_layout, obs_dtype, obs)
+            rc = self._step_obs_fn(self._hv, a.data_ptr(), r.data_ptr(), d.data_ptr(), lay, _DTYPES[o.dtype],
+                                   o.data_ptr(), st)
+            if rc:
+                L.check(rc, "oth_step_observe")
+        else:
+            o = None
+            rc = self._step_fn(self._hv, a.data_ptr(), r.data_ptr(), d.data_ptr(), st)
+            if rc:
+                L.check(rc, "oth_step")
         bv = self._bview
         if bv is None or bv[0] is not d:  # 0/1 bytes: a view, not a conversion kernel
-            bv = self._bview = (d, d.view(torch.bool))
-        return obs, r, bv[1], None
+            bv = self._bview = (d, d if d.dtype is torch.bool else d.view(torch.bool))
+        return o, r, bv[1], None
+
+    def _check_out(self, t, dtypes, name):
+        """A caller-given (E,) output the kernels write: on this device, contiguous,
+        E elements of one of `dtypes` -- else ValueError before any launch."""
+        if not isinstance(t, torch.Tensor) or t.dtype not in dtypes or t.device != self.device or \
+                not t.is_contiguous() or t.numel() != self.num_envs:
+            raise ValueError("%s must be a contiguous %s tensor of %d elements on %s" %
+                             (name, " or ".join(str(x) for x in dtypes), self.num_envs, self.device))
+
+    def _obs_shape(self, lay):
+        n = self.board_size
+        return (self.num_envs, n, n) if lay in _ONE_PLANE else (self.num_envs, _OBS_PLANES[lay], n, n)
+
+    def _obs_out(self, layout, dtype, out):
+        """(layout id, output tensor) of a fused observation: get_observation()'s
+        layout unless given; `out` checked once per tensor, or a new tensor."""
+        if layout is None:
+            lay = L.OTH_OBS_BOARD_LEGAL if self.possible_actions_in_obs else L.OTH_OBS_BOARD
+        else:
+            lay = _OBS_LAYOUTS[layout] if isinstance(layout, str) else int(layout)
+            if lay not in _OBS_PLANES:
+                raise ValueError("unknown observation layout %r" % (layout,))
+        if out is None:
+            if dtype not in _DTYPES:
+                raise ValueError("observation dtype must be one of %s" % list(_DTYPES))
+            return lay, torch.empty(self._obs_shape(lay), dtype=dtype, device=self.device)
+        ok = self._okobs
+        if ok is None or ok[0] is not out or ok[1] != lay:
+            shape = self._obs_shape(lay)
+            if out.dtype not in _DTYPES or out.device != self.device or not out.is_contiguous() or \
+                    out.numel() != _numel(shape):
+                raise ValueError("obs must be a contiguous tensor of %s elements (shape %s) of one of %s on %s" %
+                                 (_numel(shape), shape, list(_DTYPES), self.device))
+            self._okobs = (out, lay)
+        return lay, out
 
     def step_policy(self, policy="random", n_plies=1, actions=None, rewards=None, dones=None, record=True):
         """n_plies plies where every board's mover plays `policy` on the device
@@ -341,14 +397,18 @@ class VecOthelloEnv(object):
         return acts, lp, ent
 
     def sample_step(self, logits, deterministic=False, uniforms=None, log_probs=True, entropy=True,
-                    full_entropy=False, rewards=None, dones=None, actions=None):
+                    full_entropy=False, rewards=None, dones=None, actions=None, observe=None, obs=None,
+                    obs_dtype=torch.float32):
         """sample_actions(logits) then step(actions) in ONE launch (oth_sample_step):
         Policy.act (model.py:60-99) over every board's possible_moves followed by
         OthelloBaseEnv.step (othello.py:412-462), bit-identical to the two calls.
         Returns (actions int32, log_probs, entropy, rewards int32, dones bool).
         Outputs may be given to be written in place: `actions` / `rewards` int32 (E,),
         `dones` uint8 (E,), and `log_probs` / `entropy` as float32 (E,) tensors
-        instead of True."""
+        instead of True.  observe: an observation layout ('make_state', the
+        learners' next input (util.py:48-74), 'board', ...): the stepped boards'
+        observation from the same launch (oth_sample_step_observe), into `obs` if
+        given or a new `obs_dtype` tensor, appended as a sixth value."""
         x, uniforms = self._sampler_inputs(logits, uniforms)
         acts = self._out(actions, torch.int32, "actions")
         lp = self._out(log_probs, torch.float32, "log_probs")
@@ -357,11 +417,19 @@ class VecOthelloEnv(object):
         d = self._out(dones, torch.uint8, "dones")
         mode = (L.OTH_MASKED_MODE if deterministic else L.OTH_MASKED_SAMPLE) | \
             (L.OTH_MASKED_FULL_ENTROPY if full_entropy else 0)
-        L.check(self._lib.oth_sample_step(self._h, _ptr(x), x.stride(0), _ptr(uniforms), self._sample_calls, mode,
-                                          _ptr(acts), _ptr(lp), _ptr(ent), _ptr(r), _ptr(d), self._stream()),
-                "oth_sample_step")
+        if observe is None:
+            L.check(self._lib.oth_sample_step(self._h, _ptr(x), x.stride(0), _ptr(uniforms), self._sample_calls,
+                                              mode, _ptr(acts), _ptr(lp), _ptr(ent), _ptr(r), _ptr(d),
+                                              self._stream()), "oth_sample_step")
+        else:
+            lay, o = self._obs_out(observe, obs_dtype, obs)
+            L.check(self._lib.oth_sample_step_observe(self._h, _ptr(x), x.stride(0), _ptr(uniforms),
+                                                      self._sample_calls, mode, _ptr(acts), _ptr(lp), _ptr(ent),
+                                                      _ptr(r), _ptr(d), lay, _DTYPES[o.dtype], _ptr(o),
+                                                      self._stream()), "oth_sample_step_observe")
         self._sample_calls += 1
-        return acts, lp, ent, r, (d.view(torch.bool) if d is not None else None)
+        res = (acts, lp, ent, r, (d.view(torch.bool) if d is not None else None))
+        return res if observe is None else res + (o,)
 
     @property
     def sample_counter(self):
@@ -475,6 +543,13 @@ class VecOthelloEnv(object):
         _, m, _ = self.get_state()
         w = (m >> 2) & 3
         return torch.where(w == 1, WHITE_DISK, torch.where(w == 2, BLACK_DISK, NO_DISK))
+
+
+def _numel(shape):
+    k = 1
+    for x in shape:
+        k *= x
+    return k
 
 
 def _no_capture(what):

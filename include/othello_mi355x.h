@@ -112,6 +112,17 @@ int oth_reset(oth_env *env, const uint8_t *mask, oth_stream_t stream);
  * wrapper does so on the host). */
 int oth_step(oth_env *env, const int32_t *actions, int32_t *rewards, uint8_t *dones, oth_stream_t stream);
 
+/* oth_step, then the observation of the stepped boards in the same call:
+ * OthelloBaseEnv.step's returned get_observation() (othello.py:462; layout
+ * OTH_OBS_BOARD / OTH_OBS_BOARD_LEGAL) or any oth_observe layout / dtype into
+ * obs (E, planes, N, N).  The values are exactly oth_step followed by
+ * oth_observe: the state after the ply (and after an auto-reset).  One launch
+ * where the board is one word and N*N % 4 == 0 with obs aligned to 4
+ * elements (the observation is written from the registers that stepped the
+ * board, nothing read back); two launches otherwise. */
+int oth_step_observe(oth_env *env, const int32_t *actions, int32_t *rewards, uint8_t *dones, int32_t layout,
+                     int32_t dtype, void *obs, oth_stream_t stream);
+
 /* n_plies plies of on-device play: each env's mover picks with `policy`
  * (RandomPolicy.get_action simple_policies.py:37-41 / GreedyPolicy.get_action
  * :69-92, or a random move while random-opening plies remain) and steps.
@@ -222,6 +233,46 @@ int oth_sample_actions(oth_env *env, const float *logits, int64_t ld, const floa
 int oth_sample_step(oth_env *env, const float *logits, int64_t ld, const float *uniforms, uint64_t counter,
                     int32_t mode, int32_t *actions, float *log_probs, float *entropy, int32_t *rewards,
                     uint8_t *dones, oth_stream_t stream);
+
+/* oth_sample_step, then the observation of the stepped boards (layout, dtype
+ * as oth_observe: e.g. OTH_OBS_MAKE_STATE in OTH_F32, the learners' next input,
+ * util.py:48-74) into obs in the same call: bit-identical to oth_sample_step +
+ * oth_observe.  One launch for N*N % 4 == 0 with obs aligned to 4 elements. */
+int oth_sample_step_observe(oth_env *env, const float *logits, int64_t ld, const float *uniforms, uint64_t counter,
+                            int32_t mode, int32_t *actions, float *log_probs, float *entropy, int32_t *rewards,
+                            uint8_t *dones, int32_t layout, int32_t dtype, void *obs, oth_stream_t stream);
+
+/* One board's state in the reference's terms, as the single-board drop-in
+ * classes (OthelloBaseEnv / SimpleOthelloEnv / OthelloEnv, othello.py:21-501;
+ * BASELINE config 1) return it after every call.  W used words per colour. */
+#define OTH_RECORD_MAX_WORDS 4
+#define OTH_RECORD_MAX_SQUARES 256
+typedef struct oth_record {
+    uint64_t black[OTH_RECORD_MAX_WORDS]; /* the board (exchange format) */
+    uint64_t white[OTH_RECORD_MAX_WORDS];
+    uint64_t legal[OTH_RECORD_MAX_WORDS]; /* possible_moves (stale on terminal plies, as the reference's) */
+    uint32_t seq;                         /* the call's sequence number (written last) */
+    uint16_t meta;                        /* exchange-format meta: player_turn, terminated, winner */
+    uint8_t done;                         /* the step's done (0 without a step) */
+    uint8_t planes;                       /* observation planes in obs: 1, or 2 with the legal plane */
+    int32_t reward;                       /* the step's reward (0 without a step) */
+    int32_t white_cnt, black_cnt;         /* count_disks (othello.py:468-471) */
+    int32_t greedy;                       /* GreedyPolicy.get_action for the side to move (simple_policies.py:69-92);
+                                             -1 without a possible move */
+    int8_t obs[2 * OTH_RECORD_MAX_SQUARES];   /* get_observation() (othello.py:363-378): planes x N x N */
+    int8_t board_state[OTH_RECORD_MAX_SQUARES]; /* board_state (othello.py:257): white +1, black -1 */
+} oth_record;
+
+/* The single-board drop-in path in one launch and one wait: if step != 0,
+ * OthelloBaseEnv.step (othello.py:412-462) of board `board` with the host value
+ * `action` (any int: not in possible_moves takes the invalid path; a
+ * terminated board is left as it is and reports done, as oth_step), then the
+ * board's record (layout OTH_OBS_BOARD or OTH_OBS_BOARD_LEGAL for obs) is
+ * written by the same kernel into a mapped host buffer the handle owns, and the
+ * call returns once it has landed: *out points at it until the next call on
+ * this handle.  step == 0 only records (after reset / set_state / set_player_turn). */
+int oth_step_sync(oth_env *env, int32_t board, int32_t step, int32_t action, int32_t layout,
+                  const oth_record **out, oth_stream_t stream);
 
 /* Global ply counter of the handle: the Philox counter of the next eager ply
  * (random policy, openings, device opponents).  Host value only; setting it

@@ -49,6 +49,7 @@ def lib():
         L.oracle_greedy_batch.argtypes = [i32, i32, P, P, P, P]
         L.oracle_recompute_legal.argtypes = [i32, i32, P, P, P]
         L.oracle_observe.argtypes = [i32, i32, P, P, P, P, P, P]
+        L.oracle_count_disks_batch.argtypes = [i32, i32, P, P, P]
         L.oracle_maximin_batch.argtypes = [i32, i32, i32, P, P, P, P]
         L.oracle_reset_vs.argtypes = [i32, u32, i32, i32, u64, u32, u64, i32, P, P, P, P]
         L.oracle_step_vs.argtypes = [i32, u32, i32, i32, u64, u32, u64, i32, P, P, P, P, P, P, P, P, P]
@@ -203,6 +204,13 @@ def maximin(s, depth):
 def recompute_legal(s):
     out = np.zeros_like(s.legal)
     lib().oracle_recompute_legal(s.n, s.E, _p(s.boards), _p(s.meta), _p(out))
+    return out
+
+
+def count_disks(s):
+    """count_disks (othello.py:468-471) of every board: int32 (E, 2) = (white, black)."""
+    out = np.zeros((s.E, 2), dtype=np.int32)
+    lib().oracle_count_disks_batch(s.n, s.E, _p(s.boards), _p(s.meta), _p(out))
     return out
 
 

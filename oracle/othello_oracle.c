@@ -455,6 +455,20 @@ void oracle_recompute_legal(int n, int E, const uint64_t *boards, const uint16_t
     }
 }
 
+/* count_disks (othello.py:468-471) of every board: out[2i] = white, out[2i+1] = black. */
+void oracle_count_disks_batch(int n, int E, const uint64_t *boards, const uint16_t *meta, int32_t *out) {
+    int W = nwords(n);
+    oenv e;
+    uint64_t zero[MAXW] = {0};
+    for (int i = 0; i < E; i++) {
+        int w, b;
+        load(&e, n, 0, boards + (size_t)i * 2 * W, meta[i], zero);
+        count_disks(&e, &w, &b);
+        out[2 * (size_t)i] = w;
+        out[2 * (size_t)i + 1] = b;
+    }
+}
+
 /* get_observation (othello.py:363-378) as int8 (E, [2,] N, N) and
  * util.make_state (util.py:48-74) as float32 (E, 4, N, N). */
 void oracle_observe(int n, int E, const uint64_t *boards, const uint16_t *meta, const uint64_t *legal,

@@ -63,7 +63,7 @@ def test_spawned_ranks_cover_the_global_boards(world):
               "per_gpu_value", "single_gpu_same_shard", "ranks", "shared_device"):
         assert k in d, k
     assert d["n_gpus"] == world and d["ranks"] == world and d["shared_device"] is False
-    assert d["config"]["boards_per_gpu"] == 131072 and d["roofline"]["bound"] == "hbm"
+    assert d["config"]["boards_per_gpu"] == 131072 and d["roofline"]["bound"] == "valu-issue"
 
 
 def test_shared_device_rehearsal_is_labelled():

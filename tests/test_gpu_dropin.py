@@ -171,3 +171,89 @@ def test_maximin_policy_dropin(pkg, golden_dir):
             env.set_board_state(board.reshape(8, 8), perspective=1)
             env.set_player_turn(int(g[k + "turn"][i]))
             assert pol.get_action(env.get_observation()) == int(g[k + "action"][i])
+
+
+@pytest.mark.parametrize("n,E,board", [(8, 1, 0), (6, 7, 5), (10, 3, 1), (16, 2, 1), (7, 70, 64)])
+def test_step_sync_record_matches_oracle(pkg, n, E, board):
+    """oth_step_sync (the drop-in's one launch per step()): the record of board
+    `board` -- state, reward / done, count_disks, GreedyPolicy's move,
+    get_observation in both layouts, board_state -- equals the oracle after the
+    same steps (legal, illegal and out-of-range actions, both sudden-death
+    modes); the handle's other boards are untouched."""
+    import ctypes
+
+    import torch
+
+    from gymothelloenv_amd import _lib as L
+    from oracle import oracle
+    for sd in (True, False):
+        env = pkg.VecOthelloEnv(E, board_size=n, sudden_death_on_invalid_move=sd, device="cuda:0")
+        lib = env._lib
+        s = oracle.reset(n, 1)
+        b0 = [t.clone() for t in env.get_state()]
+        rng = np.random.RandomState(n + sd)
+        ptr = ctypes.c_void_p()
+        flags = oracle.F_SUDDEN_DEATH if sd else 0
+        W, nn = oracle.nwords(n), n * n
+        for p in range(n * n):
+            terminated = bool(s.meta[0] & 2)
+            legal = [a for a in range(nn) if (int(s.legal[0, a // 64]) >> (a % 64)) & 1]
+            if terminated:
+                a, step = 0, 0  # the drop-in raises instead of stepping; record only
+            else:
+                a = int(rng.choice(legal)) if legal and rng.rand() > 0.15 else int(rng.randint(-3, nn + 3))
+                step = 1
+                orw, od, _ = oracle.step(s, flags, np.array([a], dtype=np.int32))
+            layout = L.OTH_OBS_BOARD_LEGAL if p % 2 else L.OTH_OBS_BOARD
+            L.check(lib.oth_step_sync(env._h, board, step, a, layout, ctypes.byref(ptr), env._stream()),
+                    "oth_step_sync")
+            rec = L.OthRecord.from_address(ptr.value)
+            what = "%dx%d sd=%d ply %d a=%d" % (n, n, sd, p, a)
+            assert list(rec.black)[:W] == list(s.boards[0, :W]) and list(rec.white)[:W] == list(s.boards[0, W:]), what
+            assert list(rec.legal)[:W] == list(s.legal[0]), what
+            assert rec.meta == s.meta[0], what
+            if step:
+                assert (rec.reward, rec.done) == (int(orw[0]), int(od[0])), what
+            wb = oracle.count_disks(s)[0]
+            assert (rec.white_cnt, rec.black_cnt) == (wb[0], wb[1]), what
+            if not s.meta[0] & 2:  # (a terminal record's possible_moves are stale: no policy reads them)
+                now = [x for x in range(nn) if (int(s.legal[0, x // 64]) >> (x % 64)) & 1]
+                assert rec.greedy == (int(oracle.greedy(s)[0]) if now else -1), what
+            obs, obs2, _ = oracle.observe(s)
+            got = np.ctypeslib.as_array(rec.obs)[:(2 if p % 2 else 1) * nn]
+            np.testing.assert_array_equal(got, (obs2 if p % 2 else obs).reshape(-1), err_msg=what)
+            sq = np.arange(nn)
+            bits = lambda w: ((w[sq // 64] >> (sq % 64).astype(np.uint64)) & np.uint64(1)).astype(np.int8)
+            np.testing.assert_array_equal(np.ctypeslib.as_array(rec.board_state)[:nn],
+                                          bits(s.boards[0, W:]) - bits(s.boards[0, :W]), err_msg=what)
+        b1 = env.get_state()
+        others = torch.arange(E, device="cuda:0") != board
+        for x, y in zip(b0, b1):
+            assert torch.equal(x[others], y[others]), "another board changed"
+        env.close()
+
+
+def test_dropin_step_is_one_launch_per_call(pkg):
+    """The drop-in's step() costs one oth_step_sync call (no state copies, no
+    observe launches, no torch synchronisation): wall time per step well under
+    the 160-200 us of the round-4 path on a warm box, and a GreedyPolicy move
+    costs no device call at all (read from the record)."""
+    import time
+    env = pkg.OthelloBaseEnv(board_size=8, mute=True)
+    pol = pkg.GreedyPolicy()
+    pol.reset(env)
+    rnd = np.random.RandomState(0)
+    env.reset()
+    for _ in range(50):  # warm-up
+        if env.terminated:
+            env.reset()
+        env.step(pol.get_action(env.get_observation()))
+    t0, k = time.perf_counter(), 0
+    while time.perf_counter() - t0 < 0.5:
+        if env.terminated:
+            env.reset()
+        moves = env.possible_moves
+        env.step(moves[rnd.randint(0, len(moves))])
+        k += 1
+    us = (time.perf_counter() - t0) / k * 1e6
+    assert us < 100, "%.1f us per drop-in step" % us

@@ -377,6 +377,48 @@ def test_full_size_invariants(torch_cuda):
     assert 0.43 < frac[0] < 0.49 and 0.03 < frac[1] < 0.06 and 0.47 < frac[2] < 0.53
 
 
+def test_config4_shard_replays_on_oracle(torch_cuda):
+    """Config 4's per-rank workload at its real global ids: rank 7 of 8 over
+    1,048,576 boards (131,072 boards, env_id_base 917,504; the bench's weak-scaling
+    shard), 100 plies of random play with auto-reset (k_play_rand<8> at two waves
+    per SIMD), replayed by the oracle keyed by the same global ids (the
+    harnesses' W/D/L, ppo_run_self_play.py:432-441): actions, rewards, dones,
+    final state and W/D/L equal."""
+    torch = torch_cuda
+    from gymothelloenv_amd import ShardedVecOthelloEnv
+    env = ShardedVecOthelloEnv(1 << 20, rank=7, world=8, board_size=8, auto_reset=True, seed=0, device="cuda:0")
+    assert env.num_envs == 131072 and env.env_id_base == 917504
+    env.reset()
+    acts, rews, dones = env.step_policy("random", n_plies=100)
+    s = oracle.reset(8, 131072)
+    oa, orw, od, owdl = oracle.rollout_parallel(s, flags_of(True, False, True), 0, 100, seed=0, id_base=917504)
+    np.testing.assert_array_equal(acts.cpu().numpy(), oa)
+    np.testing.assert_array_equal(rews.cpu().numpy(), orw)
+    np.testing.assert_array_equal(dones.cpu().numpy(), od)
+    b, m, lg = get_state_np(env)
+    np.testing.assert_array_equal(b, s.boards)
+    np.testing.assert_array_equal(m, s.meta)
+    np.testing.assert_array_equal(lg, s.legal)
+    np.testing.assert_array_equal(env.counts().cpu().numpy(), owdl)
+    assert owdl.sum() > 131072  # every board finished at least one game
+
+
+@pytest.mark.parametrize("n", [6, 8, 10, 16])
+def test_count_disks_batched_matches_oracle(torch_cuda, n):
+    """count_disks (othello.py:468-471) of every board (k_count) on mid-game and
+    finished positions equals the oracle's, whose count is pinned to the
+    reference's disk-count rewards (test_oracle_golden)."""
+    torch = torch_cuda
+    E = 20011
+    env = make_env(torch, E, n, auto=False, seed=21)
+    for plies in (n * n // 3, n * n):  # mid-game, then most games over (boards kept terminated)
+        env.step_policy("random", n_plies=plies, record=False)
+        b, m, lg = get_state_np(env)
+        s = oracle.State(n, E)
+        s.boards[:], s.meta[:], s.legal[:] = b, m, lg
+        np.testing.assert_array_equal(env.count_disks().cpu().numpy(), oracle.count_disks(s))
+
+
 def test_state_dict_roundtrip(torch_cuda):
     torch = torch_cuda
     a = make_env(torch, 1000, 8, auto=True, seed=4)

@@ -70,6 +70,35 @@ def test_step_matches_reference_per_ply(golden_dir, n):
         np.testing.assert_array_equal(dones, t["done"][sel])
 
 
+@pytest.mark.parametrize("n", SIZES)
+def test_count_disks_matches_reference_rewards(golden_dir, n):
+    """oracle count_disks (othello.py:468-471) on every recorded post-ply board:
+    the popcounts of the reference's own board, and -- on the terminal plies of
+    the disk-reward runs that did not end by sudden death -- the reference's
+    reward, which it computes from count_disks (:444-461: mover's minus the
+    opponent's discs, N*N when the opponent has none)."""
+    t = load_traj(golden_dir, n)
+    E = len(t["action"])
+    s = oracle.State(n, E)
+    s.boards[:] = np.concatenate([t["black"], t["white"]], axis=1)
+    s.meta[:] = oracle.meta_from(t["turn"])
+    wb = oracle.count_disks(s)
+
+    def pc(words):
+        return np.array([sum(bin(int(x)).count("1") for x in row) for row in words])
+    np.testing.assert_array_equal(wb[:, 0], pc(t["white"]))
+    np.testing.assert_array_equal(wb[:, 1], pc(t["black"]))
+    dr = t["combos"][t["combo"], 1].astype(bool)
+    sudden = t["combos"][t["combo"], 0].astype(bool) & (t["reward"] == -n * n)
+    sel = t["done"] & dr & ~sudden
+    mover_white = t["prev_turn"][sel] == 1
+    mine = np.where(mover_white, wb[sel, 0], wb[sel, 1])
+    theirs = np.where(mover_white, wb[sel, 1], wb[sel, 0])
+    want = np.where(theirs == 0, n * n, mine - theirs)
+    assert sel.sum() > 0
+    np.testing.assert_array_equal(t["reward"][sel], want)
+
+
 @pytest.mark.parametrize("n", [4, 5, 8, 10, 16])
 def test_whole_games_replay(golden_dir, n):
     """Replaying each game's action list from reset reproduces every ply."""
