@@ -692,6 +692,8 @@ def side_summary(side, out):
                                                    "env_steps_per_s": _r(x["env_steps_per_s"])}
     for x in side.get("observe", []):
         summ[x["workload"]] = {"us": _r(x["avg_launch_us"]), "frac": _r(x["roofline"]["frac"])}
+    for x in side.get("maximin", []):
+        summ["policy_actions_" + x["policy"]] = {"us_per_call": x["us_per_call"], "boards": x["boards"]}
     if side.get("sustained"):
         summ["sustained"] = {k: side["sustained"][k] for k in ("seconds", "avg_launch_us", "vs_burst",
                                                                  "effective_clock_ghz")}
@@ -735,10 +737,34 @@ def vs_line(E, n, dev, stream, calls=64, opponent="random"):
     wdl = [int(x) for x in env.counts_vs()]
     env.close()
     return {"workload": "othello-env-vs-%s-%dx%d-E%d" % (opponent, n, n, E), "boards": E, "opponent": opponent,
-            "kernels": "k_policy_actions<greedy> + k_step_vs%s<%s>" % ("1" if n <= 8 else "", opponent),
+            "kernels": "k_policy_actions<greedy> + k_step_vs%s<%s>" % ("1" if n <= 8 and opponent in ("random", "greedy")
+                                                                       else "", opponent),
             "us_per_call": us,
             "plies_per_call": applied / calls, "env_steps_per_s": applied / calls / (us * 1e-6),
             "protagonist_wdl": wdl, "timing": "HIP graph of %d calls, median of 5 replays" % calls}
+
+
+def maximin_lines(E, n, dev, stream, depths=(2, 3, 4)):
+    """MaxiMinPolicy(d).get_action (simple_policies.py:98-163) for every board's
+    side to move (oth_policy_actions) on E mid-game boards (25 plies of random
+    play): depth 2 one lane per board (maximin_node), depth >= 3 a wave per
+    board (k_maximin_wave).  HIP events around `launches` back-to-back launches."""
+    import torch
+
+    from gymothelloenv_amd import VecOthelloEnv
+    env = VecOthelloEnv(E, board_size=n, auto_reset=True, seed=5, device=dev)
+    env.step_policy("random", n_plies=25, record=False)
+    out = []
+    for d in depths:
+        pol = "maximin%d" % d
+        env.policy_actions(pol)
+        launches = 5 if d >= 4 else 20
+        us = _time_launches(stream, lambda i: env.policy_actions(pol), launches)
+        out.append({"policy": pol, "boards": E, "board_size": n, "us_per_call": _r(us),
+                    "moves_per_s": _r(E / (us * 1e-6)),
+                    "kernel": "k_maximin_wave<%d>" % n if d >= 3 else "k_policy_actions<%d,maximin2>" % n})
+    env.close()
+    return out
 
 
 def single_ply(env, policy, E, W, dev, stream, k=64):
@@ -904,7 +930,8 @@ def side_measurements(env, policy, E, n, W, dev, stream, P=None, bufs=None, burs
                                          for nb in (6, 10)]}
     out["observe"] = observe_lines(n, (E, 1048576), dev, stream)
     out["configs"]["config1_single_board"] = config1_line(dev)
-    out["othello_env_vs"] = [vs_line(E, n, dev, stream, opponent=o) for o in ("random", "greedy")]
+    out["othello_env_vs"] = [vs_line(E, n, dev, stream, opponent=o) for o in ("random", "greedy", "maximin2")]
+    out["maximin"] = maximin_lines(E, n, dev, stream)
     big = VecOthelloEnv(1048576, board_size=n, auto_reset=True, seed=0, device=dev)
     big.step_policy(policy, n_plies=20, record=False)
     out["single_ply_launches"] = [single_ply(env, policy, E, W, dev, stream),

@@ -329,6 +329,19 @@ int oth_policy_actions(oth_env* env, int32_t policy, int32_t* out, oth_stream_t 
     if (!out) return fail(OTH_EINVAL, "out is NULL");
     if (policy < OTH_POLICY_GREEDY || policy > OTH_POLICY_LAST)
         return fail(OTH_EINVAL, "policy must be greedy or maximin (depth 1 .. OTH_MAXIMIN_MAX_DEPTH)");
+    if (policy >= OTH_POLICY_MAXIMIN(3)) {  // the search's size: about E x b^d leaves
+        const int d = policy - OTH_POLICY_MAXIMIN1 + 1;
+        const double b = env->n * env->n / 6.0 > 2.0 ? env->n * env->n / 6.0 : 2.0;  // a middle game's move count
+        double leaves = (double)env->E;
+        for (int i = 0; i < d; ++i) leaves *= b;
+        if (leaves > OTH_MAXIMIN_LEAF_BUDGET) {
+            char msg[200];
+            snprintf(msg, sizeof(msg), "MaxiMin depth %d over %d boards of %dx%d is ~%.1e leaves, above the "
+                     "budget of %.1e per call: split the boards over calls", d, env->E, env->n, env->n, leaves,
+                     (double)OTH_MAXIMIN_LEAF_BUDGET);
+            return fail(OTH_EINVAL, msg);
+        }
+    }
     return with_n(env->n, [&](auto NC) {
         return launch_policy_actions<decltype(NC)::value>(env, policy, out, (hipStream_t)stream);
     });

@@ -4,6 +4,7 @@
 
 #include "device.hpp"
 #include "launch.hpp"
+#include "maximin_wave.hpp"
 #include "ply.hpp"
 #include "sample_step.hpp"
 
@@ -286,11 +287,16 @@ int launch_step_vs(oth_env* env, int policy, const int32_t* actions, const int8_
     });
 }
 
+// MaxiMin of depth >= 3: one wave per board (k_maximin_wave, maximin_wave.hpp);
+// greedy and MaxiMin-2: one lane per board
 template <int N>
 int launch_policy_actions(oth_env* env, int policy, int32_t* out, hipStream_t st) {
     return with_policy(policy, [&](auto PC) {
         constexpr int POL = decltype(PC)::value;
-        if constexpr (POL != OTH_POLICY_RANDOM)
+        if constexpr (POL == OTH_POLICY_MAXIMIN3 || POL == OTH_POLICY_MAXIMIN_DEEP)
+            launch_k(k_maximin_wave<N>, dim3(env->E), dim3(64), 0, st, env->boards, env->meta, env->legal,
+                     env->E, out, POL == OTH_POLICY_MAXIMIN3 ? 3 : rng_of(env, policy).depth);
+        else if constexpr (POL != OTH_POLICY_RANDOM)
             launch_k((k_policy_actions<N, POL>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards,
                      env->meta, env->legal, env->E, out, rng_of(env, policy).depth);
         return after_launch("oth_policy_actions");

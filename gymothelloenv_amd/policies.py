@@ -75,12 +75,13 @@ class MaxiMinPolicy(object):
 
     max_search_depth <= 0: the reference's search stops at the root (depth 0 >=
     max_search_depth, :117-126) and get_action returns None -- no device call.
-    1 .. OTH_MAXIMIN_MAX_DEPTH (10): the device search.  Deeper searches raise
-    (the device's explicit stack holds 10 levels).  The search is one lane per
-    board and exponential in the depth: about b**depth leaf evaluations for b
-    moves per position (8x8 middle games: b ~ 10, so depth 7 is ~10**7 leaves
-    for ONE board, seconds of one GPU lane); DEEP_WARN_LEAVES bounds what runs
-    without a warning."""
+    1 .. OTH_MAXIMIN_MAX_DEPTH (10): the device search -- depth 3 and deeper with
+    a whole wave per board (the root's moves and their replies spread over the
+    lanes, maximin_wave.hpp).  Deeper searches raise (each lane's explicit stack
+    holds 10 levels).  The search is exponential in the depth: about b**depth
+    leaves for b moves per position (8x8 middle games: b ~ 10); the C ABI refuses
+    calls estimated above OTH_MAXIMIN_LEAF_BUDGET leaves (1.7e10), and
+    DEEP_WARN_LEAVES bounds what runs without a warning."""
 
     DEEP_WARN_LEAVES = 10 ** 6
 

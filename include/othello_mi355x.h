@@ -67,6 +67,10 @@ enum {
 #define OTH_MAXIMIN_MAX_DEPTH 10
 #define OTH_POLICY_MAXIMIN(d) (OTH_POLICY_MAXIMIN1 + (d) - 1)
 #define OTH_POLICY_LAST OTH_POLICY_MAXIMIN(OTH_MAXIMIN_MAX_DEPTH)
+/* oth_policy_actions refuses MaxiMin(d >= 3) calls whose search is estimated
+ * above this many leaves: E x b^d with b = max(2, N*N / 6) moves per position
+ * (8x8 middle games: ~10); split the boards over several calls instead */
+#define OTH_MAXIMIN_LEAF_BUDGET 17179869184.0
 
 /* observation layouts */
 enum {
@@ -166,7 +170,10 @@ int oth_greedy_actions(oth_env *env, int32_t *out, oth_stream_t stream);
 
 /* The move of a deterministic scripted policy (OTH_POLICY_GREEDY or
  * OTH_POLICY_MAXIMIN(d): MaxiMinPolicy(d).get_action, simple_policies.py:157-163)
- * for the side to move in every env; -1 where possible_moves is empty. */
+ * for the side to move in every env; -1 where possible_moves is empty.
+ * MaxiMin(d >= 3) searches each board with a whole wave (the root's moves and
+ * their replies spread over the lanes); above OTH_MAXIMIN_LEAF_BUDGET estimated
+ * leaves the call is refused (OTH_EINVAL) before anything is launched. */
 int oth_policy_actions(oth_env *env, int32_t policy, int32_t *out, oth_stream_t stream);
 
 /* Observations: layout OTH_OBS_*, dtype OTH_I8..OTH_F64, out (E, planes, N, N). */

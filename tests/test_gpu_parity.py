@@ -385,7 +385,7 @@ def test_config4_shard_replays_on_oracle(torch_cuda):
     harnesses' W/D/L, ppo_run_self_play.py:432-441): actions, rewards, dones,
     final state and W/D/L equal."""
     torch = torch_cuda
-    from gymothelloenv_amd import ShardedVecOthelloEnv
+    from gymothelloenv_amd.distributed import ShardedVecOthelloEnv
     env = ShardedVecOthelloEnv(1 << 20, rank=7, world=8, board_size=8, auto_reset=True, seed=0, device="cuda:0")
     assert env.num_envs == 131072 and env.env_id_base == 917504
     env.reset()
@@ -746,3 +746,36 @@ def test_single_ply_kernels_both_ray_sources(torch_cuda, n, E):
         np.testing.assert_array_equal(m, s.meta)
         np.testing.assert_array_equal(lg, s.legal)
         np.testing.assert_array_equal(env.counts().cpu().numpy() - wdl0, owdl)
+
+
+@pytest.mark.parametrize("n,E,depth", [(8, 256, 3), (8, 128, 4), (6, 256, 5), (4, 1024, 8), (10, 48, 4),
+                                       (8, 40, 5), (5, 300, 6)])
+def test_maximin_wave_matches_oracle(torch_cuda, n, E, depth):
+    """MaxiMin of depth >= 3 on a wave per board (k_maximin_wave: the root's moves
+    and replies over the lanes, maximin_value below) equals the oracle's search
+    (simple_policies.py:98-163 restated) on mid-game and late positions, ragged
+    E included; MaxiMin-2 (one lane per board) is unchanged."""
+    torch = torch_cuda
+    env = make_env(torch, E, n, auto=True, seed=depth + n)
+    for plies in (n * n // 3, n * n // 3):
+        env.step_policy("random", n_plies=plies, record=False)
+        b, m, lg = get_state_np(env)
+        s = oracle.State(n, E)
+        s.boards[:], s.meta[:], s.legal[:] = b, m, lg
+        got = env.policy_actions("maximin%d" % depth).cpu().numpy()
+        np.testing.assert_array_equal(got, oracle.maximin(s, depth))
+        assert (got >= 0).any()
+
+
+def test_maximin_leaf_budget_refuses_before_launch(torch_cuda):
+    """oth_policy_actions refuses a MaxiMin call whose search is estimated above
+    OTH_MAXIMIN_LEAF_BUDGET leaves (E x b^d) with a message naming the split,
+    before anything is launched; a smaller batch of the same depth runs."""
+    torch = torch_cuda
+    from gymothelloenv_amd._lib import OthelloLibError
+    env = make_env(torch, 65536, 8, auto=True, seed=1)
+    with pytest.raises(OthelloLibError, match="split the boards"):
+        env.policy_actions("maximin7")
+    small = make_env(torch, 2, 8, auto=True, seed=1)
+    small.step_policy("random", n_plies=40, record=False)
+    assert small.policy_actions("maximin5").shape == (2,)

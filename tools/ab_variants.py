@@ -33,7 +33,8 @@ def run(names, E, n, plies, launches, rounds, policy, check=True, init_rand=0):
 
     from gymothelloenv_amd import _lib as L
     from gymothelloenv_amd.vec_env import VecOthelloEnv
-    libs = {nm: L.load_path(os.path.join(VDIR, "liboth_%s.so" % nm)) for nm in names}
+    # "head": the shipped library itself
+    libs = {nm: (L.load() if nm == "head" else L.load_path(os.path.join(VDIR, "liboth_%s.so" % nm))) for nm in names}
     envs = {nm: VecOthelloEnv(E, board_size=n, auto_reset=True, seed=0, device="cuda:0", lib=lib,
                              initial_rand_steps=init_rand)
             for nm, lib in libs.items()}
