@@ -358,11 +358,16 @@ __global__ __launch_bounds__(BLOCK) void k_ply_step(uint64_t* __restrict__ board
 // store stream more waves per SIMD: at 65,536 boards the observation's store
 // loop wants four waves per SIMD (k_observe_w's 16 boards per wave), the step
 // one (k_ply_step).
+// Lane pairs with 32 boards per wave measured best at 65,536 8x8 boards (graphed,
+// us per ply; profiles/r05/a/ab_step_obs.json): int64 board 10.94 (one lane, 16
+// boards per wave) / 10.85 (one lane, 64) / 10.88 (pairs, 32); f32 make_state
+// 13.86 / 16.50 / 13.40; the two-launch form 13.01 / 16.20, the observation
+// alone 9.67 / 12.63, the step alone 3.04.
 #ifndef OTH_SO_LPB
-#define OTH_SO_LPB 1  // lanes per board of k_ply_step_obs
+#define OTH_SO_LPB 2  // lanes per board of k_ply_step_obs
 #endif
 #ifndef OTH_SO_BPW
-#define OTH_SO_BPW 16  // boards per wave of k_ply_step_obs
+#define OTH_SO_BPW 32  // boards per wave of k_ply_step_obs
 #endif
 template <int N, int LPB, int BPW>
 __global__ __launch_bounds__(BLOCK) void k_ply_step_obs(uint64_t* __restrict__ boards, uint16_t* __restrict__ meta,

@@ -7,6 +7,10 @@
 #include "device.hpp"
 #include "ply.hpp"
 
+#ifndef OTH_SS_OBS
+#define OTH_SS_OBS 1  // 0: the sample-step kernels without the observation tail (A/B of its cost when unused)
+#endif
+
 namespace oth_dev {
 
 // oth_sample_step: the learners' per-ply loop in one launch -- the masked
@@ -94,7 +98,7 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step(uint64_t* __restrict__ bo
     slot.flush();
     // oth_sample_step_observe: the wave's 64 boards' observations (lane = board)
     const long long e0 = t - (threadIdx.x & 63);
-    obs_tail<N, 64, 1>(obs_layout, obs_dtype, obs, e0, s.black.w, s.white.w, s.legal.w, s.meta,
+    if constexpr (OTH_SS_OBS) obs_tail<N, 64, 1>(obs_layout, obs_dtype, obs, e0, s.black.w, s.white.w, s.legal.w, s.meta,
                        (int)(E - e0 < 64 ? E - e0 : 64));
 }
 
@@ -191,7 +195,7 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step2(uint64_t* __restrict__ b
     // oth_sample_step_observe: the wave's 32 boards' observations (both lanes of a
     // pair hold the board as stepped and reset)
     const long long e0 = (gt - (threadIdx.x & 63)) >> 1;
-    obs_tail<N, 32, 2>(obs_layout, obs_dtype, obs, e0, s.black.w, s.white.w, s.legal.w, s.meta,
+    if constexpr (OTH_SS_OBS) obs_tail<N, 32, 2>(obs_layout, obs_dtype, obs, e0, s.black.w, s.white.w, s.legal.w, s.meta,
                        (int)(E - e0 < 32 ? E - e0 : 32));
 }
 
@@ -259,7 +263,7 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step4(uint64_t* __restrict__ b
     // oth_sample_step_observe: the wave's 16 boards' observations (the quad's four
     // lanes hold the board as stepped and reset)
     const long long e0 = (gt - (threadIdx.x & 63)) >> 2;
-    obs_tail<N, 16, 4>(obs_layout, obs_dtype, obs, e0, s.black.w, s.white.w, s.legal.w, s.meta,
+    if constexpr (OTH_SS_OBS) obs_tail<N, 16, 4>(obs_layout, obs_dtype, obs, e0, s.black.w, s.white.w, s.legal.w, s.meta,
                        (int)(E - e0 < 16 ? E - e0 : 16));
 }
 

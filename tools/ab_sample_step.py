@@ -44,7 +44,7 @@ def main():
     ref = None
     print("torch up", file=sys.stderr, flush=True)
     for nm in a.names:
-        lib = L.load_path(os.path.join(VDIR, "liboth_%s.so" % nm))
+        lib = L.load() if nm == "head" else L.load_path(os.path.join(VDIR, "liboth_%s.so" % nm))
         print("variant %s loaded" % nm, file=sys.stderr, flush=True)
         env = VecOthelloEnv(E, board_size=n, auto_reset=True, seed=0, device=dev, lib=lib)
         env.reset()
