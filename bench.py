@@ -400,7 +400,7 @@ def main(argv=None):
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, n)
         if side:
             out["side_summary"] = side_summary(side, out)  # last: a truncated tail still shows it
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out, separators=(",", ":")), flush=True)  # compact: the driver keeps a 2,000-char tail
     env.close()
     if world > 1:
         dist.destroy_process_group()

@@ -776,6 +776,10 @@ def test_maximin_leaf_budget_refuses_before_launch(torch_cuda):
     env = make_env(torch, 65536, 8, auto=True, seed=1)
     with pytest.raises(OthelloLibError, match="split the boards"):
         env.policy_actions("maximin7")
+    with pytest.raises(OthelloLibError, match="split the boards"):  # 100 searches per board
+        env.step_policy("maximin5", n_plies=100, record=False)
+    with pytest.raises(OthelloLibError, match="split the boards"):
+        env.reset_vs("maximin7")
     small = make_env(torch, 2, 8, auto=True, seed=1)
     small.step_policy("random", n_plies=40, record=False)
     assert small.policy_actions("maximin5").shape == (2,)
