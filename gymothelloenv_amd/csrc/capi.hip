@@ -124,6 +124,24 @@ __global__ __launch_bounds__(256) void k_reduce_wdl(unsigned long long* __restri
     if (threadIdx.x < 3) out[threadIdx.x] = (int64_t)acc[0][threadIdx.x];
 }
 
+// MaxiMin searches of depth >= 3 are refused above OTH_MAXIMIN_LEAF_BUDGET
+// estimated leaves per call: E x b^d x `searches` (the searches one board runs in
+// the call: plies of oth_step_policy, opponent replies of oth_step_vs), with b =
+// max(2, N*N / 6) moves per position (8x8 middle games: ~10)
+int maximin_budget(const oth_env* env, int policy, double searches) {
+    if (policy < OTH_POLICY_MAXIMIN(3) || policy > OTH_POLICY_LAST) return OTH_OK;
+    const int d = policy - OTH_POLICY_MAXIMIN1 + 1;
+    const double b = env->n * env->n / 6.0 > 2.0 ? env->n * env->n / 6.0 : 2.0;
+    double leaves = (double)env->E * searches;
+    for (int i = 0; i < d; ++i) leaves *= b;
+    if (leaves <= OTH_MAXIMIN_LEAF_BUDGET) return OTH_OK;
+    char msg[240];
+    snprintf(msg, sizeof(msg), "MaxiMin depth %d over %d boards of %dx%d (x%.0f searches) is ~%.1e leaves, above the "
+             "budget of %.1e per call: split the boards over calls", d, env->E, env->n, env->n, searches, leaves,
+             (double)OTH_MAXIMIN_LEAF_BUDGET);
+    return fail(OTH_EINVAL, msg);
+}
+
 }  // namespace
 
 extern "C" {
@@ -245,6 +263,10 @@ int oth_step_sync(oth_env* env, int32_t board, int32_t step, int32_t action, int
     if (board < 0 || board >= env->E) return fail(OTH_EINVAL, "board out of range");
     if (layout != OTH_OBS_BOARD && layout != OTH_OBS_BOARD_LEGAL)
         return fail(OTH_EINVAL, "layout must be OTH_OBS_BOARD or OTH_OBS_BOARD_LEGAL");
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    OTH_HIP(hipStreamIsCapturing((hipStream_t)stream, &cap));
+    if (cap != hipStreamCaptureStatusNone)  // it waits for its record: never inside a graph capture
+        return fail(OTH_EINVAL, "oth_step_sync waits for its result and cannot run during a stream capture");
     if (!env->rec_host) {  // mapped, coherent pinned host memory: the kernel's stores land in it directly
         void* h = nullptr;
         OTH_HIP(hipHostMalloc(&h, sizeof(oth_record), hipHostMallocMapped | hipHostMallocCoherent));
@@ -291,6 +313,7 @@ int oth_step_policy(oth_env* env, int32_t policy, int32_t n_plies, int32_t* acti
     if (n_plies < 0) return fail(OTH_EINVAL, "n_plies must be >= 0");
     if (policy < OTH_POLICY_RANDOM || policy > OTH_POLICY_LAST) return fail(OTH_EINVAL, "unknown policy");
     if (n_plies == 0) return OTH_OK;
+    if (int rc = maximin_budget(env, policy, (double)n_plies)) return rc;
     const uint64_t ply0 = env->ply;
     env->ply += (uint64_t)n_plies;
     return with_n(env->n, [&](auto NC) {
@@ -304,6 +327,7 @@ int oth_reset_vs(oth_env* env, int32_t opponent_policy, const int8_t* protagonis
     OTH_CHECK_ENV(env);
     if (opponent_policy < OTH_POLICY_RANDOM || opponent_policy > OTH_POLICY_LAST)
         return fail(OTH_EINVAL, "unknown opponent policy");
+    if (int rc = maximin_budget(env, opponent_policy, 2.0)) return rc;
     const uint64_t call = env->ply++;
     return with_n(env->n, [&](auto NC) {
         return launch_reset_vs<decltype(NC)::value>(env, opponent_policy, protagonist, mask, call,
@@ -317,6 +341,7 @@ int oth_step_vs(oth_env* env, int32_t opponent_policy, const int32_t* actions, c
     if (!actions) return fail(OTH_EINVAL, "actions is NULL");
     if (opponent_policy < OTH_POLICY_RANDOM || opponent_policy > OTH_POLICY_LAST)
         return fail(OTH_EINVAL, "unknown opponent policy");
+    if (int rc = maximin_budget(env, opponent_policy, 2.0)) return rc;
     const uint64_t call = env->ply++;
     return with_n(env->n, [&](auto NC) {
         return launch_step_vs<decltype(NC)::value>(env, opponent_policy, actions, protagonist, rewards, dones,
@@ -329,19 +354,7 @@ int oth_policy_actions(oth_env* env, int32_t policy, int32_t* out, oth_stream_t 
     if (!out) return fail(OTH_EINVAL, "out is NULL");
     if (policy < OTH_POLICY_GREEDY || policy > OTH_POLICY_LAST)
         return fail(OTH_EINVAL, "policy must be greedy or maximin (depth 1 .. OTH_MAXIMIN_MAX_DEPTH)");
-    if (policy >= OTH_POLICY_MAXIMIN(3)) {  // the search's size: about E x b^d leaves
-        const int d = policy - OTH_POLICY_MAXIMIN1 + 1;
-        const double b = env->n * env->n / 6.0 > 2.0 ? env->n * env->n / 6.0 : 2.0;  // a middle game's move count
-        double leaves = (double)env->E;
-        for (int i = 0; i < d; ++i) leaves *= b;
-        if (leaves > OTH_MAXIMIN_LEAF_BUDGET) {
-            char msg[200];
-            snprintf(msg, sizeof(msg), "MaxiMin depth %d over %d boards of %dx%d is ~%.1e leaves, above the "
-                     "budget of %.1e per call: split the boards over calls", d, env->E, env->n, env->n, leaves,
-                     (double)OTH_MAXIMIN_LEAF_BUDGET);
-            return fail(OTH_EINVAL, msg);
-        }
-    }
+    if (int rc = maximin_budget(env, policy, 1.0)) return rc;
     return with_n(env->n, [&](auto NC) {
         return launch_policy_actions<decltype(NC)::value>(env, policy, out, (hipStream_t)stream);
     });

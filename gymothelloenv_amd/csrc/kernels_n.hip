@@ -186,6 +186,12 @@ int launch_play(oth_env* env, int policy, int n_plies, int32_t* actions, int32_t
     });
 }
 
+// with the observation tail: lane quads (16 boards a wave, the store loop's best
+// shape) up to this many boards.  8x8, make_state f32, graphed: 32,768 boards
+// 14.27 -> 12.34 us per ply on quads; 65,536 17.37 -> 17.85 (profiles/r05/c/ab_ss_obs*.json)
+#ifndef OTH_SSO_QUAD_MAX_E
+#define OTH_SSO_QUAD_MAX_E 32768
+#endif
 template <int N, int G, bool VEC, bool FULL>
 void launch_ss(oth_env* env, const float* logits, long long ld, const float* uniforms, uint64_t counter, int mode,
                int32_t* actions, float* log_probs, float* entropy, int32_t* rewards, uint8_t* dones, uint64_t ply,
@@ -195,7 +201,8 @@ void launch_ss(oth_env* env, const float* logits, long long ld, const float* uni
     // beyond, the quads' duplicated step work loses to pairs (65,536: 7.02 -> 7.45)
     // (the tally slots oth_create sizes cover the quads' grid: one slot per block)
     if constexpr (Geo<N>::W == 1) {
-        if (env->E <= OTH_SS_QUAD_MAX_E && grid_for(4LL * env->E) <= env->nslots) {
+        const long long quad_max = ob.out ? OTH_SSO_QUAD_MAX_E : OTH_SS_QUAD_MAX_E;
+        if (env->E <= quad_max && grid_for(4LL * env->E) <= env->nslots) {
             launch_k((k_sample_step4<N, VEC, FULL>), dim3(grid_for(4LL * env->E)), dim3(BLOCK), 0, st,
                      env->boards, env->meta, env->legal, env->E, env->flags, logits, ld, uniforms, counter,
                      mode, actions, log_probs, entropy, rewards, dones, env->wdl, rng_of(env), ply, ob.layout, ob.dtype,

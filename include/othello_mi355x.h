@@ -67,9 +67,11 @@ enum {
 #define OTH_MAXIMIN_MAX_DEPTH 10
 #define OTH_POLICY_MAXIMIN(d) (OTH_POLICY_MAXIMIN1 + (d) - 1)
 #define OTH_POLICY_LAST OTH_POLICY_MAXIMIN(OTH_MAXIMIN_MAX_DEPTH)
-/* oth_policy_actions refuses MaxiMin(d >= 3) calls whose search is estimated
- * above this many leaves: E x b^d with b = max(2, N*N / 6) moves per position
- * (8x8 middle games: ~10); split the boards over several calls instead */
+/* oth_policy_actions, oth_step_policy and oth_reset_vs / oth_step_vs refuse
+ * MaxiMin(d >= 3) calls whose searches are estimated above this many leaves:
+ * E x b^d x the searches per board in the call (n_plies for oth_step_policy, 2
+ * opponent replies for the _vs calls) with b = max(2, N*N / 6) moves per
+ * position (8x8 middle games: ~10); split the boards over several calls */
 #define OTH_MAXIMIN_LEAF_BUDGET 17179869184.0
 
 /* observation layouts */

@@ -11,6 +11,10 @@ between launches); the per-ply time is HIP events around the replay / P.
               replay must end in the recording's state)
   play1       oth_step_policy(random, 1 ply) (k_ply_rand)
   sample_step oth_sample_step (Policy.act + step in one launch), random logits
+  step_obs    oth_step_observe: step_ext with the int64 get_observation from the
+              same launch (k_ply_step_obs)
+  step_obs_ms the same with f32 make_state
+  ss_obs      oth_sample_step_observe: sample_step with the next make_state f32
 
     python tools/prof_step.py [--envs 65536,1048576] [--plies 32] [--cases step_ext,play1,sample_step]
 """
@@ -84,6 +88,27 @@ def main():
                 return "replay_equals_recording"
             graphed("step_ext", lambda i: env.step(rec_a[i], rewards=rew, dones=don, observe=False), 40 * W + 11,
                     check=same)
+        if "step_obs" in cases or "step_obs_ms" in cases:
+            rec_a = torch.empty(P, E, dtype=torch.int32, device=dev)
+            env.set_state(b0, m0, l0)
+            env.step_policy("random", n_plies=P, actions=rec_a, record=True)
+            for case, lay, dt, per in (("step_obs", "board", torch.int64, 8 * n * n),
+                                       ("step_obs_ms", "make_state", torch.float32, 16 * n * n)):
+                if case not in cases:
+                    continue
+                ob = torch.empty((E, n, n) if lay == "board" else (E, 4, n, n), dtype=dt, device=dev)
+                graphed(case, lambda i, ob=ob, lay=lay: env.step(rec_a[i], rewards=rew, dones=don, obs=ob,
+                                                                 obs_layout=lay), 40 * W + 11 + per)
+                del ob
+        if "ss_obs" in cases:
+            g = torch.Generator(device=dev).manual_seed(0)
+            logits = torch.randn(E, n * n, device=dev, generator=g)
+            a = torch.empty(E, dtype=torch.int32, device=dev)
+            ms = torch.empty(E, 4, n, n, dtype=torch.float32, device=dev)
+            graphed("ss_obs", lambda i: env.sample_step(logits, log_probs=False, entropy=False, actions=a,
+                                                       rewards=rew, dones=don, observe="make_state", obs=ms),
+                    4 * n * n + 40 * W + 11 + 16 * n * n)
+            del ms
         if "play1" in cases:
             a1 = torch.empty(1, E, dtype=torch.int32, device=dev)
             graphed("play1", lambda i: env.step_policy("random", n_plies=1, actions=a1, rewards=rew[None],
