@@ -703,7 +703,7 @@ def side_summary(side, out):
     return summ
 
 
-def vs_line(E, n, dev, stream, calls=64, opponent="random"):
+def vs_line(E, n, dev, stream, calls=64, opponent="random", observe=False):
     """OthelloEnv's turn loop on the device (othello.py:151-200; oth_reset_vs /
     oth_step_vs): a greedy protagonist (oth_policy_actions, GreedyPolicy
     simple_policies.py:69-92) against the embedded `opponent` on E boards with
@@ -720,8 +720,10 @@ def vs_line(E, n, dev, stream, calls=64, opponent="random"):
     env.reset_vs(opponent, protagonist=1)
     plies = []  # each call's plies-applied tensor (graph memory: holds the last replay's values)
 
-    def call():
-        return env.step_vs(env.policy_actions("greedy"), opponent, observe=False)[3]
+    ob = torch.empty(E, n, n, dtype=torch.int64, device=dev) if observe else None
+
+    def call():  # observe: OthelloEnv.step's int64 obs (othello.py:200) from the same launch
+        return env.step_vs(env.policy_actions("greedy"), opponent, observe=observe, obs=ob)[3]
     for _ in range(4):
         call()
     torch.cuda.synchronize()
@@ -736,7 +738,8 @@ def vs_line(E, n, dev, stream, calls=64, opponent="random"):
     applied = int(sum(int(p.sum().item()) for p in plies))  # plies of the last replay
     wdl = [int(x) for x in env.counts_vs()]
     env.close()
-    return {"workload": "othello-env-vs-%s-%dx%d-E%d" % (opponent, n, n, E), "boards": E, "opponent": opponent,
+    return {"workload": "othello-env-vs-%s-%dx%d-E%d%s" % (opponent, n, n, E, "-obs" if observe else ""), "boards": E,
+            "opponent": opponent + ("+obs" if observe else ""),
             "kernels": "k_policy_actions<greedy> + k_step_vs%s<%s>" % ("1" if n <= 8 and opponent in ("random", "greedy")
                                                                        else "", opponent),
             "us_per_call": us,
@@ -930,7 +933,8 @@ def side_measurements(env, policy, E, n, W, dev, stream, P=None, bufs=None, burs
                                          for nb in (6, 10)]}
     out["observe"] = observe_lines(n, (E, 1048576), dev, stream)
     out["configs"]["config1_single_board"] = config1_line(dev)
-    out["othello_env_vs"] = [vs_line(E, n, dev, stream, opponent=o) for o in ("random", "greedy", "maximin2")]
+    out["othello_env_vs"] = [vs_line(E, n, dev, stream, opponent=o) for o in ("random", "greedy", "maximin2")] + \
+        [vs_line(E, n, dev, stream, opponent="random", observe=True)]
     out["maximin"] = maximin_lines(E, n, dev, stream)
     big = VecOthelloEnv(1048576, board_size=n, auto_reset=True, seed=0, device=dev)
     big.step_policy(policy, n_plies=20, record=False)

@@ -73,6 +73,7 @@ SIGNATURES = {
     "oth_step_policy": (_I32, [_P, _I32, _I32, _P, _P, _P, _P]),
     "oth_reset_vs": (_I32, [_P, _I32, _P, _P, _P]),
     "oth_step_vs": (_I32, [_P, _I32, _P, _P, _P, _P, _P, _P]),
+    "oth_step_vs_observe": (_I32, [_P, _I32, _P, _P, _P, _P, _P, _I32, _I32, _P, _P]),
     "oth_legal": (_I32, [_P, _P, _P]),
     "oth_legal_moves": (_I32, [_I32, _I32, _P, _P, _P, _P]),
     "oth_greedy_actions": (_I32, [_P, _P, _P]),

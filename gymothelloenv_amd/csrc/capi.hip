@@ -345,7 +345,24 @@ int oth_step_vs(oth_env* env, int32_t opponent_policy, const int32_t* actions, c
     const uint64_t call = env->ply++;
     return with_n(env->n, [&](auto NC) {
         return launch_step_vs<decltype(NC)::value>(env, opponent_policy, actions, protagonist, rewards, dones,
-                                                   plies, call, (hipStream_t)stream);
+                                                   plies, call, -1, 0, nullptr, (hipStream_t)stream);
+    });
+}
+
+int oth_step_vs_observe(oth_env* env, int32_t opponent_policy, const int32_t* actions, const int8_t* protagonist,
+                        int32_t* rewards, uint8_t* dones, int32_t* plies, int32_t layout, int32_t dtype, void* obs,
+                        oth_stream_t stream) {
+    OTH_CHECK_ENV(env);
+    if (!actions || !obs) return fail(OTH_EINVAL, "actions / obs is NULL");
+    if (opponent_policy < OTH_POLICY_RANDOM || opponent_policy > OTH_POLICY_LAST)
+        return fail(OTH_EINVAL, "unknown opponent policy");
+    if (layout < OTH_OBS_BOARD || layout > OTH_OBS_LEGAL) return fail(OTH_EINVAL, "unknown layout");
+    if (dtype < OTH_I8 || dtype > OTH_F64) return fail(OTH_EINVAL, "unknown dtype");
+    if (int rc = maximin_budget(env, opponent_policy, 2.0)) return rc;
+    const uint64_t call = env->ply++;
+    return with_n(env->n, [&](auto NC) {
+        return launch_step_vs<decltype(NC)::value>(env, opponent_policy, actions, protagonist, rewards, dones,
+                                                   plies, call, layout, dtype, obs, (hipStream_t)stream);
     });
 }
 

@@ -94,6 +94,13 @@ int launch_step(oth_env* env, const int32_t* actions, int32_t* rewards, uint8_t*
     return after_launch("oth_step");
 }
 
+// from this many boards oth_step_observe takes k_observe_w's large-launch shape (one
+// lane per board, 64 boards a wave) instead of lane pairs: at 1,048,576 8x8 boards
+// the pairs' launch took 125.4 us with the int64 board against 116 for the two
+// launches (profiles/r05/d/step/times.jsonl)
+#ifndef OTH_SO_LARGE_E
+#define OTH_SO_LARGE_E 262144
+#endif
 // oth_step_observe: one-word boards step and observe in one launch (k_ply_step_obs,
 // ply.hpp); other sizes, or an output the quad stores cannot write, take
 // oth_step's kernel and then oth_observe's
@@ -102,11 +109,18 @@ int launch_step_observe(oth_env* env, const int32_t* actions, int32_t* rewards, 
                         void* obs, uint64_t ply, hipStream_t st) {
     if constexpr (Geo<N>::W == 1 && (N * N) % 4 == 0) {
         if (obs_fusable<N>(dtype, obs)) {
-            constexpr int BPW = OTH_SO_BPW;
-            const long long waves = ((long long)env->E + BPW - 1) / BPW;
-            launch_k((k_ply_step_obs<N, OTH_SO_LPB, BPW>), dim3(grid_for(waves * 64)), dim3(BLOCK), 0, st,
-                     env->boards, env->meta, env->legal, env->E, env->flags, actions, rewards, dones, env->wdl,
-                     rng_of(env), ply, layout, dtype, obs);
+            if (env->E < OTH_SO_LARGE_E) {
+                constexpr int BPW = OTH_SO_BPW;
+                const long long waves = ((long long)env->E + BPW - 1) / BPW;
+                launch_k((k_ply_step_obs<N, OTH_SO_LPB, BPW>), dim3(grid_for(waves * 64)), dim3(BLOCK), 0, st,
+                         env->boards, env->meta, env->legal, env->E, env->flags, actions, rewards, dones, env->wdl,
+                         rng_of(env), ply, layout, dtype, obs);
+            } else {  // k_observe_w's large-launch shape: one lane per board, 64 boards a wave
+                const long long waves = ((long long)env->E + 63) / 64;
+                launch_k((k_ply_step_obs<N, 1, 64>), dim3(grid_for(waves * 64)), dim3(BLOCK), 0, st, env->boards,
+                         env->meta, env->legal, env->E, env->flags, actions, rewards, dones, env->wdl, rng_of(env),
+                         ply, layout, dtype, obs);
+            }
             return after_launch("oth_step_observe");
         }
     }
@@ -275,22 +289,32 @@ int launch_reset_vs(oth_env* env, int policy, const int8_t* prot, const uint8_t*
     });
 }
 
+// obs: NULL, or the observation (layout, dtype) of the boards after the call
+// (oth_step_vs_observe): from k_step_vs1's registers where its quad stores can
+// write it, else a k_observe launch after the call's kernel
 template <int N>
 int launch_step_vs(oth_env* env, int policy, const int32_t* actions, const int8_t* prot, int32_t* rewards,
-                   uint8_t* dones, int32_t* plies, uint64_t call, hipStream_t st) {
+                   uint8_t* dones, int32_t* plies, uint64_t call, int obs_layout, int obs_dtype, void* obs,
+                   hipStream_t st) {
     return with_policy(policy, [&](auto PC) {
         constexpr int POL = decltype(PC)::value;
+        bool fused = false;
         // one-word boards against a random or greedy opponent: k_step_vs1 (ply.hpp;
         // 65,536 8x8 boards 16-19 % less per call, profiles/r04/vs/)
-        if constexpr (Geo<N>::W == 1 && (POL == OTH_POLICY_RANDOM || POL == OTH_POLICY_GREEDY))
+        if constexpr (Geo<N>::W == 1 && (POL == OTH_POLICY_RANDOM || POL == OTH_POLICY_GREEDY)) {
+            fused = obs && obs_fusable<N>(obs_dtype, obs);
+            const ObsOut ob = fused ? ObsOut{obs_layout, obs_dtype, obs} : ObsOut{};
             launch_k((k_step_vs1<N, POL>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards,
                      env->meta, env->legal, env->E, env->flags, actions, prot, rewards, dones, plies,
-                     env->wdl, env->wdl_vs, rng_of(env, policy), call);
-        else
+                     env->wdl, env->wdl_vs, rng_of(env, policy), call, ob.layout, ob.dtype, ob.out);
+        } else {
             launch_k((k_step_vs<N, POL>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards,
                      env->meta, env->legal, env->E, env->flags, actions, prot, rewards, dones, plies,
                      env->wdl, env->wdl_vs, rng_of(env, policy), call);
-        return after_launch("oth_step_vs");
+        }
+        const int rc = after_launch("oth_step_vs");
+        if (rc || !obs || fused) return rc;
+        return launch_observe<N>(env, obs_layout, obs_dtype, obs, st);
     });
 }
 
@@ -412,7 +436,7 @@ template int launch_step<OTH_N>(oth_env*, const int32_t*, int32_t*, uint8_t*, ui
 template int launch_play<OTH_N>(oth_env*, int, int, int32_t*, int32_t*, uint8_t*, uint64_t, hipStream_t);
 template int launch_reset_vs<OTH_N>(oth_env*, int, const int8_t*, const uint8_t*, uint64_t, hipStream_t);
 template int launch_step_vs<OTH_N>(oth_env*, int, const int32_t*, const int8_t*, int32_t*, uint8_t*, int32_t*,
-                                   uint64_t, hipStream_t);
+                                   uint64_t, int, int, void*, hipStream_t);
 template int launch_sample_step<OTH_N>(oth_env*, const float*, long long, const float*, uint64_t, int, int32_t*,
                                        float*, float*, int32_t*, uint8_t*, uint64_t, int, int, void*, hipStream_t);
 template int launch_step_observe<OTH_N>(oth_env*, const int32_t*, int32_t*, uint8_t*, int, int, void*, uint64_t,

@@ -87,7 +87,8 @@ int launch_reset_vs(oth_env* env, int policy, const int8_t* prot, const uint8_t*
                     hipStream_t st);
 template <int N>
 int launch_step_vs(oth_env* env, int policy, const int32_t* actions, const int8_t* prot, int32_t* rewards,
-                   uint8_t* dones, int32_t* plies, uint64_t call, hipStream_t st);
+                   uint8_t* dones, int32_t* plies, uint64_t call, int obs_layout, int obs_dtype, void* obs,
+                   hipStream_t st);
 template <int N>
 int launch_step_observe(oth_env* env, const int32_t* actions, int32_t* rewards, uint8_t* dones, int layout, int dtype,
                         void* obs, uint64_t ply, hipStream_t st);

@@ -378,6 +378,7 @@ __global__ __launch_bounds__(BLOCK) void k_ply_step_obs(uint64_t* __restrict__ b
                                                         int layout, int dtype, void* __restrict__ obs) {
     static_assert(Geo<N>::W == 1, "one-word boards");
     static_assert((LPB == 1 || LPB == 2) && LPB * BPW <= 64 && BPW >= 16, "lanes per board, boards per wave");
+    // (BPW >= 16: ceil(E / BPW) waves fit the handle's ceil(4E / 64) W/D/L slots)
     constexpr int NN = N * N;
     constexpr int RAYS = LPB == 2 ? RAYS_PAIR : RAYS_MATH;
     ply += *rng.ply_off;  // graph-region offset (oth_graph_end); 0 eagerly
@@ -461,7 +462,8 @@ __global__ __launch_bounds__(BLOCK) void k_step_vs1(uint64_t* __restrict__ board
                                                     const int8_t* __restrict__ prot, int32_t* __restrict__ rewards,
                                                     uint8_t* __restrict__ dones, int32_t* __restrict__ plies_out,
                                                     unsigned long long* __restrict__ wdl,
-                                                    unsigned long long* __restrict__ wdl_vs, Rng rng, uint64_t call) {
+                                                    unsigned long long* __restrict__ wdl_vs, Rng rng, uint64_t call,
+                                                    int obs_layout, int obs_dtype, void* __restrict__ obs) {
     static_assert(Geo<N>::W == 1, "one-word boards");
     static_assert(POLICY == OTH_POLICY_RANDOM || POLICY == OTH_POLICY_GREEDY, "random or greedy opponent");
     constexpr int NN = N * N;
@@ -472,13 +474,17 @@ __global__ __launch_bounds__(BLOCK) void k_step_vs1(uint64_t* __restrict__ board
     // after different numbers of opponent plies), read with the first loads
     WaveSlot slot(wdl, e, E), slot_vs(wdl_vs, e, E);
     uint32_t cb = 0, cd = 0, cw = 0, pw_n = 0, pd_n = 0, pl_n = 0;
+    uint64_t B = 0, Wt = 0, L = 0;  // the board after the call (the observation tail's)
+    uint32_t m = 0;
     if (e < E) {
         const uint32_t id = rng.id_base + (uint32_t)e;
         const bool pw = prot ? prot[e] == WHITE_DISK : true;
         const uint64_t gbase = call * VS_PLIES_PER_CALL;
         const ulonglong2 bw = reinterpret_cast<const ulonglong2*>(boards)[e];
-        uint64_t B = bw.x, Wt = bw.y, L = legal[e];
-        uint32_t m = meta[e];
+        B = bw.x;
+        Wt = bw.y;
+        L = legal[e];
+        m = meta[e];
         int act = actions[e];
         uint32_t j = 0;
         int r = 0, d = 1, win = NO_DISK, plies = 0;
@@ -581,6 +587,10 @@ __global__ __launch_bounds__(BLOCK) void k_step_vs1(uint64_t* __restrict__ board
     slot.flush();
     slot_vs.count(pw_n != 0, pd_n != 0, pl_n != 0);
     slot_vs.flush();
+    // oth_step_vs_observe: the wave's 64 boards' observations, the protagonist to move
+    const long long e0 = e - (int)(threadIdx.x & 63);
+    const uint64_t ob[1] = {B}, ow[1] = {Wt}, ol[1] = {L};
+    obs_tail<N, 64, 1>(obs_layout, obs_dtype, obs, e0, ob, ow, ol, m, (int)(E - e0 < 64 ? E - e0 : 64));
 }
 
 // oth_create: the handle's tables in device memory: the ray table (fill_rays<N,

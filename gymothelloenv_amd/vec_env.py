@@ -261,17 +261,29 @@ class VecOthelloEnv(object):
                 "oth_reset_vs")
         return self.get_observation()
 
-    def step_vs(self, actions, opponent="random", protagonist=None, observe=True):
+    def step_vs(self, actions, opponent="random", protagonist=None, observe=True, obs=None, obs_layout=None,
+                obs_dtype=torch.int64):
         """OthelloEnv.step (othello.py:176-200) for every board: the protagonist
         plays `actions`, the device opponent replies until the protagonist is to
         move again.  Returns (obs, rewards (protagonist's view, negated after an
-        opponent ply ended the game), dones bool, plies applied per board)."""
+        opponent ply ended the game), dones bool, plies applied per board).  The
+        observation (get_observation's layout unless `obs_layout`; into `obs` if
+        given) comes from the same launch (oth_step_vs_observe)."""
         prot = self._protagonist(protagonist)
         a = actions.to(device=self.device, dtype=torch.int32).contiguous()
+        if a.numel() != self.num_envs:
+            raise ValueError("expected %d actions, got %d" % (self.num_envs, a.numel()))
         r, d, n = self._i32(self.num_envs), self._u8(self.num_envs), self._i32(self.num_envs)
-        L.check(self._lib.oth_step_vs(self._h, _POLICIES[opponent], _ptr(a), _ptr(prot), _ptr(r), _ptr(d),
-                                      _ptr(n), self._stream()), "oth_step_vs")
-        return (self.get_observation() if observe else None), r, d.view(torch.bool), n
+        if observe:
+            lay, o = self._obs_out(obs_layout, obs_dtype, obs)
+            L.check(self._lib.oth_step_vs_observe(self._h, _POLICIES[opponent], _ptr(a), _ptr(prot), _ptr(r),
+                                                  _ptr(d), _ptr(n), lay, _DTYPES[o.dtype], _ptr(o), self._stream()),
+                    "oth_step_vs_observe")
+        else:
+            o = None
+            L.check(self._lib.oth_step_vs(self._h, _POLICIES[opponent], _ptr(a), _ptr(prot), _ptr(r), _ptr(d),
+                                          _ptr(n), self._stream()), "oth_step_vs")
+        return o, r, d.view(torch.bool), n
 
     def legal_mask(self):
         """possible_moves of every board as (E, W) int64 bit masks (bit a = square a)."""

@@ -156,6 +156,14 @@ int oth_reset_vs(oth_env *env, int32_t opponent_policy, const int8_t *protagonis
                  oth_stream_t stream);
 int oth_step_vs(oth_env *env, int32_t opponent_policy, const int32_t *actions, const int8_t *protagonist,
                 int32_t *rewards, uint8_t *dones, int32_t *plies, oth_stream_t stream);
+/* oth_step_vs, then the observation (layout / dtype as oth_observe) of the
+ * boards as the call leaves them -- OthelloEnv.step's returned obs
+ * (othello.py:200) with OTH_OBS_BOARD -- into obs in the same call: one launch
+ * for one-word boards against a random or greedy opponent with obs aligned to 4
+ * elements, else two. */
+int oth_step_vs_observe(oth_env *env, int32_t opponent_policy, const int32_t *actions, const int8_t *protagonist,
+                        int32_t *rewards, uint8_t *dones, int32_t *plies, int32_t layout, int32_t dtype, void *obs,
+                        oth_stream_t stream);
 
 /* possible_moves of every env as masks uint64[E][W] (othello.py:242, :270, :466). */
 int oth_legal(oth_env *env, uint64_t *out, oth_stream_t stream);

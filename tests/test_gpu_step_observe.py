@@ -102,13 +102,14 @@ def test_step_observe_every_layout_and_dtype(torch_cuda, n, E):
         env.close()
 
 
-@pytest.mark.parametrize("n,E", [(8, 65536), (6, 4099)])
+@pytest.mark.parametrize("n,E", [(8, 65536), (6, 4099), (8, 262147)])
 def test_step_observe_equals_two_calls_and_default_layout(torch_cuda, n, E):
     """The fused call against oth_step + oth_observe on a twin handle: equal
     rewards, dones, state, W/D/L and observation; the default observation is
     get_observation()'s (board, or board_legal with possible_actions_in_obs);
     an output one element past the vector alignment takes the two-launch path
-    with the same values; preallocated outputs are written in place."""
+    with the same values; preallocated outputs are written in place.  From
+    262,144 boards the fused launch takes one lane per board, 64 boards a wave."""
     torch = torch_cuda
     from gymothelloenv_amd import VecOthelloEnv
     for pa in (False, True):
@@ -140,6 +141,34 @@ def test_step_observe_equals_two_calls_and_default_layout(torch_cuda, n, E):
         assert int(fused.counts().sum()) > 0 or E < 10
         fused.close()
         split.close()
+
+
+def test_step_observe_large_launch_every_layout(torch_cuda):
+    """From 262,144 boards the fused launch takes one lane per board and 64 boards
+    a wave (k_ply_step_obs<8, 1, 64>): every layout and dtype equal to oth_step
+    + oth_observe on a twin handle (compared on the device), 262,147 boards."""
+    torch = torch_cuda
+    from gymothelloenv_amd import VecOthelloEnv
+    E, n = 262147, 8
+    kw = dict(board_size=n, auto_reset=True, seed=6, device="cuda:0")
+    fused, split = VecOthelloEnv(E, **kw), VecOthelloEnv(E, **kw)
+    rng = np.random.RandomState(3)
+    s = oracle.reset(n, E)
+    combos = [(lay, dt) for lay in LAYOUTS for dt in _dtypes(torch)]
+    for p, (lay, dt) in enumerate(combos):
+        acts = mixed_actions(rng, s, n)
+        oracle.step(s, oracle.F_SUDDEN_DEATH | oracle.F_AUTO_RESET, acts, seed=6, ply=p)
+        a = torch.from_numpy(acts).cuda()
+        o1, r1, d1, _ = fused.step(a, obs_layout=lay, obs_dtype=dt)
+        _, r2, d2, _ = split.step(a, observe=False)
+        o2 = split.observe(lay, dt)
+        assert torch.equal(o1, o2) and torch.equal(r1, r2) and torch.equal(d1, d2), "ply %d %s %s" % (p, lay, dt)
+    b, m, lg = state_np(fused)
+    np.testing.assert_array_equal(b, s.boards)
+    np.testing.assert_array_equal(m, s.meta)
+    np.testing.assert_array_equal(lg, s.legal)
+    fused.close()
+    split.close()
 
 
 @pytest.mark.parametrize("n", [8, 6])
@@ -232,3 +261,33 @@ def test_step_output_buffers_checked(torch_cuda):
         obs, rr, dd, _ = env.step(a, rewards=r, dones=d, obs=o, obs_layout="make_state")
         assert obs is o and rr is r
     env.close()
+
+
+@pytest.mark.parametrize("n,opp,E", [(8, "random", 65536), (8, "greedy", 4099), (6, "random", 3000),
+                                     (10, "greedy", 2000), (8, "maximin2", 1000)])
+def test_step_vs_observe_equals_two_calls(torch_cuda, n, opp, E):
+    """OthelloEnv.step on the device with its returned observation (othello.py:200)
+    from the same launch (k_step_vs1 + the observation tail; the generic k_step_vs
+    and a k_observe launch for two-word boards and MaxiMin opponents): every
+    layout equal to oth_step_vs + oth_observe on a twin handle, mixed protagonist
+    colours, random openings, auto-reset."""
+    torch = torch_cuda
+    from gymothelloenv_amd import VecOthelloEnv
+    kw = dict(board_size=n, auto_reset=True, seed=12, initial_rand_steps=4, device="cuda:0")
+    fused, split = VecOthelloEnv(E, **kw), VecOthelloEnv(E, **kw)
+    prot = torch.from_numpy(np.where(np.arange(E) % 3 == 0, -1, 1).astype(np.int8))
+    o1 = fused.reset_vs(opp, protagonist=prot)
+    o2 = split.reset_vs(opp, protagonist=prot)
+    assert torch.equal(o1, o2)
+    for c in range(12):
+        acts = fused.policy_actions("greedy")
+        lay, dt = LAYOUTS[c % len(LAYOUTS)], _dtypes(torch)[c % 5]
+        o1, r1, d1, p1 = fused.step_vs(acts, opp, obs_layout=lay, obs_dtype=dt)
+        _, r2, d2, p2 = split.step_vs(acts, opp, observe=False)
+        o2 = split.observe(lay, dt)
+        what = "%s %dx%d call %d %s %s" % (opp, n, n, c, lay, dt)
+        assert torch.equal(r1, r2) and torch.equal(d1, d2) and torch.equal(p1, p2), what
+        assert o1.dtype == dt and torch.equal(o1, o2), what
+    for x, y in zip(fused.get_state(), split.get_state()):
+        assert torch.equal(x, y)
+    assert torch.equal(fused.counts_vs(), split.counts_vs())
