@@ -25,7 +25,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 SIZES = list(range(4, 17))
 SOURCES = ("capi.hip", "kernels_n.hip", "play_rand_n.hip", "masked.hip", "device.hpp", "launch.hpp", "bitboard.hpp",
-           "masked.hpp", "ply.hpp", "sample_step.hpp", "pair_play.hpp", "maximin_wave.hpp")
+           "masked.hpp", "ply.hpp", "sample_step.hpp", "maximin_wave.hpp")
 PLAY_SIZES = list(range(4, 12))  # k_play_rand (one-word boards) and k_play_rand_w (two-word boards)
 # play_rand_n.hip: the max-ILP machine scheduler (one wave per SIMD: latency hidden by the schedule
 # counts, occupancy does not); the rest of the library keeps the default scheduler

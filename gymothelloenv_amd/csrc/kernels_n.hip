@@ -260,7 +260,7 @@ int launch_sample_step(oth_env* env, const float* logits, long long ld, const fl
     const int base = mode & 3;
     // the observation from the step kernel's registers where its quad stores can
     // write `obs`; else a k_observe launch after it (the same values)
-    const bool fuse = OTH_SS_OBS && obs && obs_fusable<N>(obs_dtype, obs);
+    const bool fuse = obs && obs_fusable<N>(obs_dtype, obs);
     const ObsOut ob = fuse ? ObsOut{obs_layout, obs_dtype, obs} : ObsOut{};
     if (vec) {
         if (full) launch_ss<N, G, true, true>(env, logits, ld, uniforms, counter, base, actions, log_probs, entropy,
@@ -318,16 +318,16 @@ int launch_step_vs(oth_env* env, int policy, const int32_t* actions, const int8_
     });
 }
 
-// MaxiMin of depth >= 3: one wave per board (k_maximin_wave, maximin_wave.hpp);
-// greedy and MaxiMin-2: one lane per board
-#ifndef OTH_MAXIMIN_WAVE
-#define OTH_MAXIMIN_WAVE 1  // 0: every depth one lane per board (maximin_node / maximin_search; A/B)
-#endif
+// MaxiMin of depth >= 3: one wave per board (k_maximin_wave, maximin_wave.hpp;
+// against one lane per board, 65,536 8x8 boards: depth 3 786 -> 348 us, depth 4
+// 19.9 -> 4.7 ms; profiles/r05/b/ab_maximin.jsonl); greedy and MaxiMin-2: one
+// lane per board
+
 template <int N>
 int launch_policy_actions(oth_env* env, int policy, int32_t* out, hipStream_t st) {
     return with_policy(policy, [&](auto PC) {
         constexpr int POL = decltype(PC)::value;
-        if constexpr (OTH_MAXIMIN_WAVE && (POL == OTH_POLICY_MAXIMIN3 || POL == OTH_POLICY_MAXIMIN_DEEP))
+        if constexpr (POL == OTH_POLICY_MAXIMIN3 || POL == OTH_POLICY_MAXIMIN_DEEP)
             launch_k(k_maximin_wave<N>, dim3(env->E), dim3(64), 0, st, env->boards, env->meta, env->legal,
                      env->E, out, POL == OTH_POLICY_MAXIMIN3 ? 3 : rng_of(env, policy).depth);
         else if constexpr (POL != OTH_POLICY_RANDOM)

@@ -9,11 +9,6 @@
 // the fused sample-and-step kernel 4 %, hence the separate unit.
 #include "device.hpp"
 #include "launch.hpp"
-#include "pair_play.hpp"
-
-#ifndef OTH_GREEDY_PAIR
-#define OTH_GREEDY_PAIR 0  // 1: greedy play on lane pairs (k_play_greedy2, pair_play.hpp)
-#endif
 
 #ifndef OTH_N
 #error "compile with -DOTH_N=<board size>"
@@ -29,11 +24,9 @@ void launch_play_rand(oth_env* env, int n_plies, int32_t* actions, int32_t* rewa
                       hipStream_t st) {
     const dim3 grid((unsigned)(((long long)env->E + BLOCK - 1) / BLOCK)), block(BLOCK);
     const Rng rng{env->seed, env->id_base, env->init_rand, env->cur_off};
-    if constexpr (Geo<N>::W == 1 && POL == OTH_POLICY_GREEDY && OTH_GREEDY_PAIR)
-        launch_k((k_play_greedy2<N>), dim3((unsigned)((2LL * env->E + BLOCK - 1) / BLOCK)), block, 0, st,
-                 env->boards, env->meta, env->legal, env->E, env->flags, n_plies, actions, rewards, dones, env->wdl,
-                 rng, ply0, env->rays);
-    else if constexpr (Geo<N>::W == 1)
+    // (greedy play on lane pairs, k_play_greedy2, measured 7 % slower and was removed:
+    // git show 53fb080:gymothelloenv_amd/csrc/pair_play.hpp)
+    if constexpr (Geo<N>::W == 1)
         launch_k((k_play_rand<N, POL>), grid, block, 0, st, env->boards, env->meta, env->legal, env->E,
                  env->flags, n_plies, actions, rewards, dones, env->wdl, rng, ply0, env->rays);
     else  // random play only (k_play_rand_w)

@@ -7,9 +7,8 @@
 #include "device.hpp"
 #include "ply.hpp"
 
-#ifndef OTH_SS_OBS
-#define OTH_SS_OBS 1  // 0: the sample-step kernels without the observation tail (A/B of its cost when unused)
-#endif
+// (the observation tail at the end of the three kernels costs nothing when unused:
+// 65,536 8x8 boards 5.99 -> 6.03 us per graphed ply, profiles/r05/b/ab_ss_tail.json)
 
 namespace oth_dev {
 
@@ -98,7 +97,7 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step(uint64_t* __restrict__ bo
     slot.flush();
     // oth_sample_step_observe: the wave's 64 boards' observations (lane = board)
     const long long e0 = t - (threadIdx.x & 63);
-    if constexpr (OTH_SS_OBS) obs_tail<N, 64, 1>(obs_layout, obs_dtype, obs, e0, s.black.w, s.white.w, s.legal.w, s.meta,
+    obs_tail<N, 64, 1>(obs_layout, obs_dtype, obs, e0, s.black.w, s.white.w, s.legal.w, s.meta,
                        (int)(E - e0 < 64 ? E - e0 : 64));
 }
 
@@ -195,7 +194,7 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step2(uint64_t* __restrict__ b
     // oth_sample_step_observe: the wave's 32 boards' observations (both lanes of a
     // pair hold the board as stepped and reset)
     const long long e0 = (gt - (threadIdx.x & 63)) >> 1;
-    if constexpr (OTH_SS_OBS) obs_tail<N, 32, 2>(obs_layout, obs_dtype, obs, e0, s.black.w, s.white.w, s.legal.w, s.meta,
+    obs_tail<N, 32, 2>(obs_layout, obs_dtype, obs, e0, s.black.w, s.white.w, s.legal.w, s.meta,
                        (int)(E - e0 < 32 ? E - e0 : 32));
 }
 
@@ -263,7 +262,7 @@ __global__ __launch_bounds__(BLOCK) void k_sample_step4(uint64_t* __restrict__ b
     // oth_sample_step_observe: the wave's 16 boards' observations (the quad's four
     // lanes hold the board as stepped and reset)
     const long long e0 = (gt - (threadIdx.x & 63)) >> 2;
-    if constexpr (OTH_SS_OBS) obs_tail<N, 16, 4>(obs_layout, obs_dtype, obs, e0, s.black.w, s.white.w, s.legal.w, s.meta,
+    obs_tail<N, 16, 4>(obs_layout, obs_dtype, obs, e0, s.black.w, s.white.w, s.legal.w, s.meta,
                        (int)(E - e0 < 16 ? E - e0 : 16));
 }
 

@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
 """MaxiMinPolicy(d) for every board (oth_policy_actions) in the shipped library
-(depth >= 3 on a wave per board, k_maximin_wave) against a variant built with
--DOTH_MAXIMIN_WAVE=0 (one lane walking each board's tree): identical moves
+(depth >= 3 on a wave per board, k_maximin_wave) against a variant where every
+depth ran one lane per board (the OTH_MAXIMIN_WAVE=0 switch of commit 53fb080,
+removed after this A/B: profiles/r05/b/ab_maximin.jsonl): identical moves
 first, then interleaved HIP-event timings, on mid-game boards.
 
-    python tools/ab_variants.py --sizes 8 --build mmlane=-DOTH_MAXIMIN_WAVE=0   # here
+    git checkout 53fb080 && python tools/ab_variants.py --sizes 8 --build mmlane=-DOTH_MAXIMIN_WAVE=0
     python tools/ab_maximin.py mmlane [--envs 65536 --depths 3 4]                # GPU box
 """
 import argparse
