@@ -1766,7 +1766,8 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const uint64_t* __restrict__ 
 }
 
 // A quad of 4 consecutive squares of one plane as one vector store (16 B for
-// f32 / i32, 4 B for i8, 2 x 16 B for the 8-byte types): k_observe_w's unit.
+// f32 / i32, 4 B for i8, 2 x 16 B for the 8-byte types): k_observe_w's unit
+// (the 8-byte types take pairs of squares instead, OTH_OBS_PAIR8).
 // (as streaming stores: 65,536 boards 2-3 % slower, 1,048,576 int64 boards 104 -> 250 us;
 // profiles/r04/d/ab_obs_nt.jsonl)
 template <typename T>
@@ -1795,6 +1796,14 @@ __device__ __forceinline__ void put_quad(T* out, uint32_t q, int v0, int v1, int
     }
 }
 
+#ifndef OTH_OBS_PAIR8
+// 8-byte observations by pairs of squares, one 16-B store per lane (1 KiB
+// contiguous per store instruction) instead of quads in two 16-B stores (each
+// instruction half of a 2-KiB span): oth_step_observe with its int64 board at
+// 65,536 8x8 boards 11.05 -> 8.80 us per graphed ply (torch's fill_ of the same
+// tensor: 8.95; profiles/r05/i/ab_step_obs.json)
+#define OTH_OBS_PAIR8 1
+#endif
 template <int LAYOUT>
 constexpr int obs_planes() {
     return LAYOUT == OTH_OBS_BOARD_LEGAL ? 2 : (LAYOUT == OTH_OBS_MAKE_STATE ? 4 : 1);
@@ -1855,11 +1864,19 @@ __device__ __forceinline__ void obs_stream(const uint64_t (&bw)[Geo<N>::W], cons
     // unrolled by 4 +-0 (by 2 / 4 on the branch-free body: +-0, profiles/r04/obs/ab_unroll_bf.jsonl); 128 / 256 boards per wave (every wave resident at once, all
     // loads first) 218.8 -> 216.6 / 234.4, and at 262,144 boards 46.5 -> 57.6 / 110.3
     // (profiles/r04/obs/)
-    for (int g0 = 0; g0 < total; g0 += 64) {
-        const uint32_t g = (uint32_t)(g0 + lane < total ? g0 + lane : total - 1);
-        const uint32_t kb = g / PQ, rr = g - kb * PQ;
-        const uint32_t plane = rr / Q, q = rr - plane * Q;
-        const uint32_t a0 = 4 * q, wi = a0 / 64, bi = a0 % 64;  // 4 | 64: a quad never straddles words
+    // S squares per lane and store: quads (S = 4), or for the 8-byte types under
+    // OTH_OBS_PAIR8 pairs (S = 2: one 16-B store per lane, so each store
+    // instruction writes 1 KiB contiguous instead of two half-filled 2-KiB spans)
+    constexpr int S = (sizeof(T) == 8 && OTH_OBS_PAIR8) ? 2 : 4;
+    constexpr uint32_t UQ = (uint32_t)(NN / S), UB = (uint32_t)obs_planes<LAYOUT>() * UQ;  // units per plane / board
+    constexpr uint32_t SM = (1u << S) - 1u;
+    const int totalu = nb * (int)UB;
+    (void)total;
+    for (int g0 = 0; g0 < totalu; g0 += 64) {
+        const uint32_t g = (uint32_t)(g0 + lane < totalu ? g0 + lane : totalu - 1);
+        const uint32_t kb = g / UB, rr = g - kb * UB;
+        const uint32_t plane = rr / UQ, q = rr - plane * UQ;
+        const uint32_t a0 = S * q, wi = a0 / 64, bi = a0 % 64;  // S | 64: a unit never straddles words
         const uint64_t xb = fetch(bw, (int)kb, (int)wi), xw = fetch(ww, (int)kb, (int)wi);
         const uint32_t flk = (uint32_t)__shfl((int)fl, (int)kb * LS);
         const bool tw = (flk & 1u) != 0;
@@ -1871,33 +1888,43 @@ __device__ __forceinline__ void obs_stream(const uint64_t (&bw)[Geo<N>::W], cons
         // between them): make_state f32 at 65,536 / 262,144 / 1,048,576 boards
         // 13.75 -> 12.79 / 46.6 -> 41.5 / 219.8 -> 208.3 us, int64 board 1,048,576
         // 104.7 -> 102.4 (profiles/r04/obs/ab_branchfree.jsonl)
-        int v[4];
+        int v[4] = {0, 0, 0, 0};
         if constexpr (LAYOUT == OTH_OBS_LEGAL) {  // possible_moves
-            const uint32_t nl = (uint32_t)(xl >> bi) & 0xFu;
+            const uint32_t nl = (uint32_t)(xl >> bi) & SM;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = (int)((nl >> j) & 1u);
+            for (int j = 0; j < S; ++j) v[j] = (int)((nl >> j) & 1u);
         } else if constexpr (LAYOUT == OTH_OBS_ABSOLUTE) {  // othello.py:257
-            const uint32_t nbk = (uint32_t)(xb >> bi) & 0xFu, nwk = (uint32_t)(xw >> bi) & 0xFu;
+            const uint32_t nbk = (uint32_t)(xb >> bi) & SM, nwk = (uint32_t)(xw >> bi) & SM;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = (int)((nwk >> j) & 1u) - (int)((nbk >> j) & 1u);
+            for (int j = 0; j < S; ++j) v[j] = (int)((nwk >> j) & 1u) - (int)((nbk >> j) & 1u);
         } else if constexpr (LAYOUT == OTH_OBS_MAKE_STATE) {  // util.py:48-74
             const uint64_t m0 = 0ull - (uint64_t)(plane == 0u), m1 = 0ull - (uint64_t)(plane == 1u);
             const uint64_t m2 = 0ull - (uint64_t)(plane == 2u && tw), m3 = 0ull - (uint64_t)(plane == 3u && (flk & 2u));
-            const uint32_t bits = (uint32_t)(((xb & m0) | (xw & m1) | (xl & m3) | m2) >> bi) & 0xFu;
+            const uint32_t bits = (uint32_t)(((xb & m0) | (xw & m1) | (xl & m3) | m2) >> bi) & SM;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = (int)((bits >> j) & 1u);
+            for (int j = 0; j < S; ++j) v[j] = (int)((bits >> j) & 1u);
         } else {  // othello.py:363-376: mover +1, opponent -1; plane 1 the legal squares
             const uint64_t xm = tw ? xw : xb, xo = tw ? xb : xw;
-            const uint32_t mv = (uint32_t)(xm >> bi) & 0xFu, op = (uint32_t)(xo >> bi) & 0xFu;
-            const uint32_t nl = (uint32_t)(xl >> bi) & 0xFu;
+            const uint32_t mv = (uint32_t)(xm >> bi) & SM, op = (uint32_t)(xo >> bi) & SM;
+            const uint32_t nl = (uint32_t)(xl >> bi) & SM;
             const bool p1 = plane != 0u;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < S; ++j) {
                 const int b = (int)((mv >> j) & 1u) - (int)((op >> j) & 1u);
                 v[j] = p1 ? (int)((nl >> j) & 1u) : b;
             }
         }
-        if (g0 + lane < total) put_quad<T>(base, (uint32_t)g, v[0], v[1], v[2], v[3]);
+        if (g0 + lane < totalu) {
+            if constexpr (S == 2) {
+                using V2 = typename std::conditional<std::is_same<T, double>::value, double2, longlong2>::type;
+                V2 x;
+                x.x = (T)v[0];
+                x.y = (T)v[1];
+                reinterpret_cast<V2*>(base)[g] = x;
+            } else {
+                put_quad<T>(base, g, v[0], v[1], v[2], v[3]);
+            }
+        }
     }
 }
 

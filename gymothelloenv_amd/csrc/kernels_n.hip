@@ -327,9 +327,12 @@ template <int N>
 int launch_policy_actions(oth_env* env, int policy, int32_t* out, hipStream_t st) {
     return with_policy(policy, [&](auto PC) {
         constexpr int POL = decltype(PC)::value;
-        if constexpr (POL == OTH_POLICY_MAXIMIN3 || POL == OTH_POLICY_MAXIMIN_DEEP)
-            launch_k(k_maximin_wave<N>, dim3(env->E), dim3(64), 0, st, env->boards, env->meta, env->legal,
-                     env->E, out, POL == OTH_POLICY_MAXIMIN3 ? 3 : rng_of(env, policy).depth);
+        if constexpr (POL == OTH_POLICY_MAXIMIN3 || POL == OTH_POLICY_MAXIMIN_DEEP) {
+            const int depth = POL == OTH_POLICY_MAXIMIN3 ? 3 : rng_of(env, policy).depth;
+            constexpr bool NEST = Geo<N>::W <= 2;  // (boards of 3+ words: maximin_value either way)
+            auto k = depth >= 4 && env->E <= OTH_MM_NESTED_MAX_E ? k_maximin_wave<N, NEST> : k_maximin_wave<N, false>;
+            launch_k(k, dim3(env->E), dim3(64), 0, st, env->boards, env->meta, env->legal, env->E, out, depth);
+        }
         else if constexpr (POL != OTH_POLICY_RANDOM)
             launch_k((k_policy_actions<N, POL>), dim3(grid_for(env->E)), dim3(BLOCK), 0, st, env->boards,
                      env->meta, env->legal, env->E, out, rng_of(env, policy).depth);

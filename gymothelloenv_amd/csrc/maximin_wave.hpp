@@ -16,6 +16,17 @@
 
 #include "device.hpp"
 
+#ifndef OTH_MM_NESTED_MAX_E
+// launches of at most this many boards at depth >= 4 take the nested subtrees
+// (maximin_node: 342 VGPRs, one wave per SIMD); larger launches and depth 3 the
+// explicit stack (maximin_value), whose lower register count keeps more boards'
+// waves resident.  8x8, nested against the explicit stack: depth 4 at 1,024 /
+// 4,096 / 16,384 / 65,536 boards 189 / 434 / 1,363 / 4,951 us against 252 / 515 /
+// 1,347 / 4,570; depth 5 at 256 / 4,096 boards 2.51 / 7.17 ms against 3.52 / 8.51;
+// one board at depth 6 36.1 against 48.8 ms (profiles/r05/i, profiles/r05/j)
+#define OTH_MM_NESTED_MAX_E 8192
+#endif
+
 namespace oth_dev {
 
 // maximin_search's best VALUE at a node whose mover is the searching side (its
@@ -79,6 +90,30 @@ __device__ int maximin_value(const BB<Geo<N>::W>& P0, const BB<Geo<N>::W>& O0, c
     return SV[0];
 }
 
+// maximin_value for a subtree depth known only at run time: boards of up to two
+// words take maximin_node's compile-time recursion (each level's state in
+// registers) for depths 2..8, instead of maximin_value's explicit stack, whose
+// dynamically indexed levels live in scratch memory
+static_assert(OTH_MAXIMIN_MAX_DEPTH - 2 <= 8, "subtree_value's compile-time depths");
+template <int N, bool NESTED>
+__device__ __forceinline__ int subtree_value(const BB<Geo<N>::W>& P, const BB<Geo<N>::W>& O,
+                                             const BB<Geo<N>::W>& L, int D) {
+    if constexpr (NESTED && Geo<N>::W <= 2) {
+        int unused;
+        switch (D) {
+            case 2: return maximin_node<N, 2, 0>(P, O, L, unused);  // (D >= 2: depth 3 ends at the planes)
+            case 3: return maximin_node<N, 3, 0>(P, O, L, unused);
+            case 4: return maximin_node<N, 4, 0>(P, O, L, unused);
+            case 5: return maximin_node<N, 5, 0>(P, O, L, unused);
+            case 6: return maximin_node<N, 6, 0>(P, O, L, unused);
+            case 7: return maximin_node<N, 7, 0>(P, O, L, unused);
+            default: return maximin_node<N, 8, 0>(P, O, L, unused);  // (D <= OTH_MAXIMIN_MAX_DEPTH - 2 = 8)
+        }
+    } else {
+        return maximin_value<N>(P, O, L, D);
+    }
+}
+
 // the k-th (0-based, ascending) set square of a multi-word mask
 template <int W>
 __device__ __forceinline__ BB<W> kth_square(const BB<W>& x, int k) {
@@ -103,7 +138,7 @@ __device__ __forceinline__ int square_of(const BB<W>& m) {
 constexpr int MW_MAX_ROOT = 64;  // root moves held per board (more: one lane searches alone)
 
 // One board per wave (block = one wave), depth D >= 3.
-template <int N>
+template <int N, bool NESTED>
 __global__ __launch_bounds__(64) void k_maximin_wave(const uint64_t* __restrict__ boards,
                                                      const uint16_t* __restrict__ meta,
                                                      const uint64_t* __restrict__ legal, int E,
@@ -170,7 +205,7 @@ __global__ __launch_bounds__(64) void k_maximin_wave(const uint64_t* __restrict_
             const BB<W> L3 = legal_moves_fills<N>(R, Q, t3);
             if (any(L3)) {
                 if (D == 3) v = popcount(R) + 1 + PlanesW<N>::max_flips(t3, L3);  // maximin_search's last level
-                else v = maximin_value<N>(R, Q, L3, D - 2);
+                else v = subtree_value<N, NESTED>(R, Q, L3, D - 2);
             }
         }
         atomicMin(&minv[i], v);

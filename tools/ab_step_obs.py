@@ -8,7 +8,8 @@ oth_observe) and the parts alone, in ONE process, at 65,536 boards:
 
 Each timing is a HIP graph of P launches replaying P plies of recorded random
 play (all legal, auto-reset) from the same start state, median of 5 replays per
-round, rounds interleaved over the variants.  Every variant's observations and
+round, rounds interleaved over the variants; "torch/fill" is torch's fill_ of
+the same observation tensor, the store-only floor.  Every variant's observations and
 final state must equal the shipped library's (checked first)."""
 import argparse
 import json
@@ -90,11 +91,18 @@ def main():
         for i in range(P):
             env.step(acts[i], rewards=rew, dones=don, observe=False)
     graphs[("head", "step_only", "-")] = g
+    # the floor: torch's own fill of the same observation tensor (a store-only kernel)
+    for lay, dt in forms:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for i in range(P):
+                outs[("head", lay)].fill_(1)
+        graphs[("torch", "fill", lay)] = g
     times = {key: [] for key in graphs}
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for r in range(a.rounds + 1):
         for key, g in graphs.items():
-            envs[key[0]].set_state(b0, m0, l0)
+            envs.get(key[0], envs["head"]).set_state(b0, m0, l0)
             reps = []
             for _ in range(5):
                 torch.cuda.synchronize()
