@@ -6,6 +6,9 @@ variant must write the same values (checked first).
 
     python tools/ab_variants.py --build old=-DOTH_OBS_SMALL_E=0 new=       # here (CPU, hipcc)
     python tools/ab_observe.py old new [--envs 65536,1048576 --launches 50 --rounds 6]   # GPU box
+
+("head" is the shipped library; torch_fill, torch's fill_ of the same tensor, is
+timed beside them; --no-check times probes that write other values.)
 """
 import argparse
 import json
@@ -25,6 +28,8 @@ def main():
     ap.add_argument("--board-size", type=int, default=8)
     ap.add_argument("--launches", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--no-check", action="store_true", help="time variants that write other values (probes)")
+    ap.add_argument("--layouts", default="board,make_state")
     a = ap.parse_args()
     import torch
 
@@ -32,14 +37,17 @@ def main():
     from gymothelloenv_amd import _lib as L
     from gymothelloenv_amd.vec_env import VecOthelloEnv
     dev = torch.device("cuda", 0)
-    libs = {nm: L.load_path(os.path.join(VDIR, "liboth_%s.so" % nm)) for nm in a.names}
+    libs = {nm: L.load() if nm == "head" else L.load_path(os.path.join(VDIR, "liboth_%s.so" % nm)) for nm in a.names}
     n = a.board_size
     for E in [int(x) for x in a.envs.split(",")]:
         envs = {nm: VecOthelloEnv(E, board_size=n, auto_reset=True, seed=3, device=dev, lib=lib)
                 for nm, lib in libs.items()}
         for env in envs.values():
             env.step_policy("random", n_plies=25, record=False)
-        for layout, dt, esize in (("board", torch.int64, 8), ("make_state", torch.float32, 4)):
+        forms = {"board": torch.int64, "make_state": torch.float32}
+        for layout in a.layouts.split(","):
+            dt = forms[layout]
+            esize = torch.empty(0, dtype=dt).element_size()
             shape = (E, n, n) if layout == "board" else (E, 4, n, n)
             bufs = {nm: torch.empty(shape, dtype=dt, device=dev) for nm in a.names}
             ref = None
@@ -47,17 +55,22 @@ def main():
                 env.observe(layout, dt, out=bufs[nm])
                 if ref is None:
                     ref = bufs[nm].clone()
-                assert torch.equal(bufs[nm], ref), "variant %s writes other values" % nm
-            graphs = {}
+                assert a.no_check or torch.equal(bufs[nm], ref), "variant %s writes other values" % nm
+            graphs = {"torch_fill": None}
             for nm, env in envs.items():
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     for _ in range(a.launches):
                         env.observe(layout, dt, out=bufs[nm])
                 graphs[nm] = g
-            times = {nm: [] for nm in a.names}
+            g = torch.cuda.CUDAGraph()  # the store floor: torch's fill_ of the same tensor
+            with torch.cuda.graph(g):
+                for _ in range(a.launches):
+                    bufs[a.names[0]].fill_(1)
+            graphs["torch_fill"] = g
+            times = {nm: [] for nm in graphs}
             for r in range(a.rounds + 1):
-                for nm in a.names:
+                for nm in graphs:
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     torch.cuda.synchronize()
                     e0.record()
