@@ -1877,6 +1877,9 @@ __device__ __forceinline__ void obs_stream(const uint64_t (&bw)[Geo<N>::W], cons
         const uint32_t kb = g / UB, rr = g - kb * UB;
         const uint32_t plane = rr / UQ, q = rr - plane * UQ;
         const uint32_t a0 = S * q, wi = a0 / 64, bi = a0 % 64;  // S | 64: a unit never straddles words
+        // (a probe storing values made from g alone, nothing fetched: k_observe_w at 65,536 /
+        // 1,048,576 boards, make_state f32 13.1 -> 12.5 / 208.7 -> 187.3 us, int64 board
+        // 7.9 -> 7.8 / 100.5 -> 89.8; profiles/r05/l/ab_obs_cst.jsonl)
         const uint64_t xb = fetch(bw, (int)kb, (int)wi), xw = fetch(ww, (int)kb, (int)wi);
         const uint32_t flk = (uint32_t)__shfl((int)fl, (int)kb * LS);
         const bool tw = (flk & 1u) != 0;
@@ -1933,10 +1936,11 @@ __device__ __forceinline__ void obs_stream(const uint64_t (&bw)[Geo<N>::W], cons
 // boards' output region (obs_stream).  One board per wave (round 2's
 // k_observe_q, each wave waiting on its own board's loads before one 1-KiB
 // store) reached 2.6 TB/s for make_state f32 at 1,048,576 boards; one wave's
-// loads feeding 64 boards' stores, 5.0 (a plain fill: 6.9).  BPW boards per wave
-// (64, or 16 for small launches: four times the waves, each streaming a quarter
+// loads feeding 64 boards' stores, 5.0 (a plain fill: 6.9).  BPW boards per wave:
+// 16 below 262,144 boards (four times the waves of 64, each streaming a quarter
 // of the region, so the store streams start sooner and more of them are in
-// flight).
+// flight); from there as many as fill about 4 KiB of output (launch_observe_w:
+// make_state f32 at 1,048,576 boards 5.3 -> 6.0 TB/s with 4 boards a wave).
 template <int N, int LAYOUT, typename T, int BPW = 64>
 __global__ __launch_bounds__(BLOCK) void k_observe_w(const uint64_t* __restrict__ boards,
                                                      const uint16_t* __restrict__ meta,

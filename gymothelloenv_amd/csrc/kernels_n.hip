@@ -101,6 +101,10 @@ int launch_step(oth_env* env, const int32_t* actions, int32_t* rewards, uint8_t*
 #ifndef OTH_SO_LARGE_E
 #define OTH_SO_LARGE_E 262144
 #endif
+// (the two launches instead from 262,144 boards, with k_observe_w's 4-KiB waves,
+// at 1,048,576 8x8 boards: the step with its int64 board 112.6 -> 115.2 us, with
+// make_state f32 216.6 -> 209.0, the learners' ply with make_state 268.7 -> 290.2;
+// profiles/r05/m)
 // oth_step_observe: one-word boards step and observe in one launch (k_ply_step_obs,
 // ply.hpp); other sizes, or an output the quad stores cannot write, take
 // oth_step's kernel and then oth_observe's
@@ -115,7 +119,7 @@ int launch_step_observe(oth_env* env, const int32_t* actions, int32_t* rewards, 
                 launch_k((k_ply_step_obs<N, OTH_SO_LPB, BPW>), dim3(grid_for(waves * 64)), dim3(BLOCK), 0, st,
                          env->boards, env->meta, env->legal, env->E, env->flags, actions, rewards, dones, env->wdl,
                          rng_of(env), ply, layout, dtype, obs);
-            } else {  // k_observe_w's large-launch shape: one lane per board, 64 boards a wave
+            } else {  // one lane per board, 64 boards a wave
                 const long long waves = ((long long)env->E + 63) / 64;
                 launch_k((k_ply_step_obs<N, 1, 64>), dim3(grid_for(waves * 64)), dim3(BLOCK), 0, st, env->boards,
                          env->meta, env->legal, env->E, env->flags, actions, rewards, dones, env->wdl, rng_of(env),
@@ -352,39 +356,43 @@ int launch_legal_moves(int n, const uint64_t* mover, const uint64_t* opp, uint64
 #ifndef OTH_OBS_SMALL_E
 #define OTH_OBS_SMALL_E 262144
 #endif
+// from OTH_OBS_SMALL_E boards: as many boards per wave (4..64) as fill about
+// OTH_OBS_LARGE_REGION bytes of output.  1,048,576 8x8 boards, 64 boards a wave
+// (every layout) against 4 KiB: int64 board 100.0 -> 94.8 us, make_state f32
+// 208.5 -> 183.6 (torch's fill_ of the same tensors: 81.6 / 157.2); regions of
+// 2 / 8 KiB: 108.0 / 102.2 and 183.2 / 197.6 (profiles/r05/l, profiles/r05/m)
+#ifndef OTH_OBS_LARGE_REGION
+#define OTH_OBS_LARGE_REGION 4096
+#endif
+template <int N, int LAYOUT, typename T>
+constexpr int obs_large_bpw() {
+    constexpr int want = OTH_OBS_LARGE_REGION / (obs_planes<LAYOUT>() * N * N * (int)sizeof(T));
+    return want >= 64 ? 64 : (want >= 32 ? 32 : (want >= 16 ? 16 : (want >= 8 ? 8 : 4)));
+}
 
 // one wave per BPW boards (k_observe_w), vector stores of 4 squares: N*N % 4 == 0
-template <int N, typename T, int BPW>
+template <int N, typename T, bool LARGE>
 void launch_observe_bpw(oth_env* env, int layout, T* o, hipStream_t st) {
-    const dim3 gw(grid_for(((long long)env->E + BPW - 1) / BPW * 64));
+    auto go = [&](auto LC) {
+        constexpr int LAY = decltype(LC)::value;
+        constexpr int BPW = LARGE ? obs_large_bpw<N, LAY, T>() : 16;
+        const dim3 gw(grid_for(((long long)env->E + BPW - 1) / BPW * 64));
+        launch_k((k_observe_w<N, LAY, T, BPW>), gw, dim3(BLOCK), 0, st, env->boards, env->meta, env->legal, env->E,
+                 o);
+    };
     switch (layout) {
-        case OTH_OBS_BOARD:
-            launch_k((k_observe_w<N, OTH_OBS_BOARD, T, BPW>), gw, dim3(BLOCK), 0, st, env->boards,
-                     env->meta, env->legal, env->E, o);
-            break;
-        case OTH_OBS_BOARD_LEGAL:
-            launch_k((k_observe_w<N, OTH_OBS_BOARD_LEGAL, T, BPW>), gw, dim3(BLOCK), 0, st, env->boards,
-                     env->meta, env->legal, env->E, o);
-            break;
-        case OTH_OBS_MAKE_STATE:
-            launch_k((k_observe_w<N, OTH_OBS_MAKE_STATE, T, BPW>), gw, dim3(BLOCK), 0, st, env->boards,
-                     env->meta, env->legal, env->E, o);
-            break;
-        case OTH_OBS_ABSOLUTE:
-            launch_k((k_observe_w<N, OTH_OBS_ABSOLUTE, T, BPW>), gw, dim3(BLOCK), 0, st, env->boards,
-                     env->meta, env->legal, env->E, o);
-            break;
-        default:
-            launch_k((k_observe_w<N, OTH_OBS_LEGAL, T, BPW>), gw, dim3(BLOCK), 0, st, env->boards,
-                     env->meta, env->legal, env->E, o);
-            break;
+        case OTH_OBS_BOARD: go(std::integral_constant<int, OTH_OBS_BOARD>{}); break;
+        case OTH_OBS_BOARD_LEGAL: go(std::integral_constant<int, OTH_OBS_BOARD_LEGAL>{}); break;
+        case OTH_OBS_MAKE_STATE: go(std::integral_constant<int, OTH_OBS_MAKE_STATE>{}); break;
+        case OTH_OBS_ABSOLUTE: go(std::integral_constant<int, OTH_OBS_ABSOLUTE>{}); break;
+        default: go(std::integral_constant<int, OTH_OBS_LEGAL>{}); break;
     }
 }
 template <int N, typename T>
 void launch_observe_w(oth_env* env, int layout, void* out, hipStream_t st) {
     T* o = static_cast<T*>(out);
-    if (env->E < OTH_OBS_SMALL_E) launch_observe_bpw<N, T, 16>(env, layout, o, st);
-    else launch_observe_bpw<N, T, 64>(env, layout, o, st);
+    if (env->E < OTH_OBS_SMALL_E) launch_observe_bpw<N, T, false>(env, layout, o, st);
+    else launch_observe_bpw<N, T, true>(env, layout, o, st);
 }
 
 template <int N>

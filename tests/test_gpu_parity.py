@@ -645,8 +645,8 @@ def test_observation_kernels_every_layout_and_alignment(torch_cuda, n):
 @pytest.mark.parametrize("n,E", [(8, 65536), (8, 262144), (6, 100003), (10, 70000)])
 def test_observation_kernels_at_size(torch_cuda, n, E):
     """k_observe_w's two wave shapes (16 boards per wave below 262,144 boards,
-    64 from there) at the configs' sizes and ragged E: int64 BOARD and f32
-    MAKE_STATE equal the numpy restatement."""
+    about 4 KiB of output per wave from there) at the configs' sizes and ragged
+    E: int64 BOARD and f32 MAKE_STATE equal the numpy restatement."""
     torch = torch_cuda
     env = make_env(torch, E, n, auto=True, seed=8)
     env.step_policy("random", n_plies=n * n // 2 + 1, record=False)
@@ -654,6 +654,22 @@ def test_observation_kernels_at_size(torch_cuda, n, E):
     for layout, dt in (("board", torch.int64), ("make_state", torch.float32), ("legal", torch.int8)):
         np.testing.assert_array_equal(env.observe(layout, dt).cpu().numpy(), _obs_np(n, b, m, lg, layout),
                                       err_msg="%s %s" % (layout, dt))
+
+
+@pytest.mark.parametrize("n,E", [(8, 262147), (6, 300001)])
+def test_observation_large_launches_every_layout_and_dtype(torch_cuda, n, E):
+    """From 262,144 boards k_observe_w takes as many boards per wave as fill
+    about 4 KiB of output (4 for make_state f32, 8 for the int64 board, up to 64
+    for int8): every layout and dtype at ragged E equal the numpy restatement."""
+    torch = torch_cuda
+    env = make_env(torch, E, n, auto=True, seed=12)
+    env.step_policy("random", n_plies=n * n // 2 + 3, record=False)
+    b, m, lg = get_state_np(env)
+    for layout in ("board", "board_legal", "make_state", "absolute", "legal"):
+        want = _obs_np(n, b, m, lg, layout)
+        for dt in (torch.int8, torch.int32, torch.int64, torch.float32, torch.float64):
+            got = env.observe(layout, dt).cpu().numpy()
+            np.testing.assert_array_equal(got, want.astype(got.dtype), err_msg="%s %s" % (layout, dt))
 
 
 @pytest.mark.parametrize("n,opp", [(8, "random"), (6, "greedy")])
