@@ -227,6 +227,9 @@ def test_sample_step_observe(torch_cuda, n, E, lay, dt):
         np.testing.assert_array_equal(r1.cpu().numpy(), orw, err_msg=what)
         np.testing.assert_array_equal(o1.cpu().numpy(), oracle_obs(s, lay).astype(o1.cpu().numpy().dtype),
                                       err_msg=what)
+    for x, y in zip(fused.get_state(), split.get_state()):
+        assert torch.equal(x, y)
+    assert torch.equal(fused.counts(), split.counts())  # the per-wave W/D/L slots
     fused.close()
     split.close()
 
