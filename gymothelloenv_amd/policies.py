@@ -77,8 +77,10 @@ class MaxiMinPolicy(object):
     max_search_depth, :117-126) and get_action returns None -- no device call.
     1 .. OTH_MAXIMIN_MAX_DEPTH (10): the device search -- depth 3 and deeper with
     a whole wave per board (the root's moves and their replies spread over the
-    lanes, maximin_wave.hpp).  Deeper searches raise (each lane's explicit stack
-    holds 10 levels).  The search is exponential in the depth: about b**depth
+    lanes, maximin_wave.hpp).  Deeper: the same search at depth = the board's
+    empty squares, which it equals (every level places a disc), once the board
+    has at most 10 empty squares; earlier in the game such a move raises
+    (VecOthelloEnv.policy_actions).  The search is exponential in the depth: about b**depth
     leaves for b moves per position (8x8 middle games: b ~ 10); the C ABI refuses
     calls estimated above OTH_MAXIMIN_LEAF_BUDGET leaves (1.7e10), and
     DEEP_WARN_LEAVES bounds what runs without a warning."""
@@ -86,9 +88,6 @@ class MaxiMinPolicy(object):
     DEEP_WARN_LEAVES = 10 ** 6
 
     def __init__(self, max_search_depth=1):
-        from ._lib import OTH_MAXIMIN_MAX_DEPTH
-        if int(max_search_depth) > OTH_MAXIMIN_MAX_DEPTH:
-            raise ValueError("max_search_depth must be at most %d on the device" % OTH_MAXIMIN_MAX_DEPTH)
         self.env = None
         self.max_search_depth = int(max_search_depth)
 

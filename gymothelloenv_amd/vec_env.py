@@ -302,8 +302,27 @@ class VecOthelloEnv(object):
         return self.policy_actions("greedy")
 
     def policy_actions(self, policy="greedy"):
-        """The move of a scripted policy ('greedy', 'maximin1'..'maximin10';
-        simple_policies.py:57-163) for the side to move on every board."""
+        """The move of a scripted policy ('greedy', 'maximin<d>'; simple_policies.py:57-163)
+        for the side to move on every board.
+
+        MaxiMin accepts any depth, as the reference does (:101-103).  Every search
+        level places a disc, so a search deeper than a board's empty squares is the
+        search of depth = its empty squares (the board is full, hence terminal, at
+        that level either way, :117-126).  Beyond OTH_MAXIMIN_MAX_DEPTH the call
+        therefore runs at the largest empty-square count of the batch's live
+        boards when that is at most OTH_MAXIMIN_MAX_DEPTH (bit-identical), and
+        raises otherwise."""
+        if isinstance(policy, str) and policy.startswith("maximin") and policy not in _POLICIES:
+            d = int(policy[len("maximin"):])
+            # (a terminated board's search returns no move at the root, whatever the depth)
+            live = ~self.terminated()
+            left = self.board_size ** 2 - self.count_disks().sum(1)
+            empties = int(left[live].max()) if bool(live.any()) else 0
+            if empties > L.OTH_MAXIMIN_MAX_DEPTH:
+                raise ValueError("maximin%d: a board has %d empty squares; the device search covers depths up to "
+                                 "%d, or any depth once every board has at most %d empty squares"
+                                 % (d, empties, L.OTH_MAXIMIN_MAX_DEPTH, L.OTH_MAXIMIN_MAX_DEPTH))
+            policy = "maximin%d" % max(1, min(d, empties))
         out = self._i32(self.num_envs)
         L.check(self._lib.oth_policy_actions(self._h, _POLICIES[policy], _ptr(out), self._stream()),
                 "oth_policy_actions")

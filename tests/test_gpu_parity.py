@@ -788,6 +788,26 @@ def test_maximin_wave_matches_oracle(torch_cuda, n, E, depth):
         assert (got >= 0).any()
 
 
+@pytest.mark.parametrize("n,E,plies,depth", [(6, 300, 24, 20), (4, 500, 5, 12), (8, 64, 52, 60)])
+def test_maximin_any_depth_by_empty_squares(torch_cuda, n, E, plies, depth):
+    """MaxiMin deeper than OTH_MAXIMIN_MAX_DEPTH, as the reference allows
+    (simple_policies.py:101-103): on boards with at most 10 empty squares the
+    search runs at the batch's largest empty-square count, which every deeper
+    search equals (each level places a disc); equal to the oracle's search at
+    the full depth.  Earlier in the game the call raises."""
+    torch = torch_cuda
+    env = make_env(torch, E, n, auto=False, seed=depth + n)
+    with pytest.raises(ValueError, match="empty squares"):
+        env.policy_actions("maximin%d" % depth)  # the start position: n*n - 4 > 10 empty squares
+    env.step_policy("random", n_plies=plies, record=False)
+    b, m, lg = get_state_np(env)
+    s = oracle.State(n, E)
+    s.boards[:], s.meta[:], s.legal[:] = b, m, lg
+    got = env.policy_actions("maximin%d" % depth).cpu().numpy()
+    np.testing.assert_array_equal(got, oracle.maximin(s, depth))
+    assert (got >= 0).any()
+
+
 def test_maximin_leaf_budget_refuses_before_launch(torch_cuda):
     """oth_policy_actions refuses a MaxiMin call whose search is estimated above
     OTH_MAXIMIN_LEAF_BUDGET leaves (E x b^d) with a message naming the split,
