@@ -10,7 +10,8 @@ any board), against the oracle restatement on the same positions:
   * the observation layouts (othello.py:257,363-376; util.py:48-74) and
     count_disks (:468-471);
   * GreedyPolicy and MaxiMin-2 / -3 (simple_policies.py:69-163);
-  * multi-ply random and greedy play with auto-reset from such positions.
+  * multi-ply random and greedy play with auto-reset from such positions;
+  * OthelloEnv.step on the device against random and greedy opponents.
 
 Hypothesis draws the board size, the disc densities and the seed of the
 position generator (derandomized: the same examples every run, no example
@@ -198,3 +199,45 @@ def test_play_from_arbitrary_positions(torch_cuda, n, seed, db, dw, policy, disk
     np.testing.assert_array_equal(m, s.meta)
     np.testing.assert_array_equal(lg, s.legal)
     np.testing.assert_array_equal(env.counts().cpu().numpy(), owdl)
+
+
+def _vs_env(n):
+    from gymothelloenv_amd import VecOthelloEnv
+    if ("vs", n) not in _PLAY:
+        _PLAY[("vs", n)] = VecOthelloEnv(E, board_size=n, auto_reset=True, seed=91, device="cuda:0")
+    return _PLAY[("vs", n)]
+
+
+@settings(**SETTINGS)
+@given(opp=st.sampled_from(["random", "greedy"]), **position)
+def test_step_vs_from_arbitrary_positions(torch_cuda, n, seed, db, dw, opp):
+    """OthelloEnv.step on the device (oth_step_vs_observe: the protagonist's
+    action, the device opponent's replies until the protagonist moves again,
+    -reward after an opponent ply ended the game, auto-reset; othello.py:176-200)
+    from arbitrary positions with the side to move as the protagonist, legal
+    and illegal actions: rewards, dones, plies, state and the returned
+    observation equal the oracle's."""
+    torch = torch_cuda
+    s = _positions(n, seed, db, min(dw, 1.0 - db))
+    prot = np.where(s.meta & 1, 1, -1).astype(np.int8)
+    env = _vs_env(n)
+    _load(torch, env, s)
+    call = env.ply_counter
+    rng = np.random.RandomState(seed ^ 0x7777)
+    acts = rng.randint(-1, n * n, size=E).astype(np.int32)
+    for e in range(E):
+        sq = [a for a in range(n * n) if (int(s.legal[e, a // 64]) >> (a % 64)) & 1]
+        if sq and rng.rand() < 0.8:
+            acts[e] = sq[rng.randint(len(sq))]
+    o, r, d, pl = env.step_vs(torch.from_numpy(acts).cuda(), opponent=opp, protagonist=torch.from_numpy(prot).cuda(),
+                              obs_layout="board")
+    orw, od, opl = oracle.step_vs(s, oracle.F_SUDDEN_DEATH | oracle.F_AUTO_RESET, 0 if opp == "random" else 1,
+                                  call, acts, seed=91, prot=prot)
+    np.testing.assert_array_equal(r.cpu().numpy(), orw)
+    np.testing.assert_array_equal(d.cpu().numpy(), od.astype(bool))
+    np.testing.assert_array_equal(pl.cpu().numpy(), opl)
+    b, m, lg = _state_np(env)
+    np.testing.assert_array_equal(b, s.boards)
+    np.testing.assert_array_equal(m, s.meta)
+    np.testing.assert_array_equal(lg, s.legal)
+    np.testing.assert_array_equal(o.cpu().numpy(), oracle.observe(s)[0].astype(np.int64))
