@@ -61,7 +61,7 @@ def main():
         for k in range(K):
             res = ply(k)
             got += [t.clone() for t in res[:4]] + [res[5].clone()]
-        got += [t.clone() for t in env.get_state()]
+        got += [t.clone() for t in env.get_state()] + [env.counts().clone()]
         if ref is None:
             ref = got
         else:
