@@ -523,8 +523,10 @@ def step_external(E, n, dev, stream, plies=64):
     rew = torch.empty(E, dtype=torch.int32, device=dev)
     don = torch.empty(E, dtype=torch.uint8, device=dev)
 
+    rows = list(acts.unbind(0))  # one action tensor per ply, as a policy hands them over (no indexing in the loop)
+
     def replay(i):
-        env.step(acts[i], rewards=rew, dones=don, observe=False)
+        env.step(rows[i], rewards=rew, dones=don, observe=False)
 
     def matches():
         b2, m2, l2 = env.get_state()
