@@ -1939,8 +1939,9 @@ __device__ __forceinline__ void obs_stream(const uint64_t (&bw)[Geo<N>::W], cons
 // loads feeding 64 boards' stores, 5.0 (a plain fill: 6.9).  BPW boards per wave:
 // 16 below 262,144 boards (four times the waves of 64, each streaming a quarter
 // of the region, so the store streams start sooner and more of them are in
-// flight); from there as many as fill about 4 KiB of output (launch_observe_w:
-// make_state f32 at 1,048,576 boards 5.3 -> 6.0 TB/s with 4 boards a wave).
+// flight); from there 64, and once the output exceeds 384 MiB as many as fill
+// about 4 KiB of output (launch_observe_w: make_state f32 at 1,048,576 boards
+// 5.3 -> 6.0 TB/s with 4 boards a wave).
 template <int N, int LAYOUT, typename T, int BPW = 64>
 __global__ __launch_bounds__(BLOCK) void k_observe_w(const uint64_t* __restrict__ boards,
                                                      const uint16_t* __restrict__ meta,

@@ -356,11 +356,19 @@ int launch_legal_moves(int n, const uint64_t* mover, const uint64_t* opp, uint64
 #ifndef OTH_OBS_SMALL_E
 #define OTH_OBS_SMALL_E 262144
 #endif
-// from OTH_OBS_SMALL_E boards: as many boards per wave (4..64) as fill about
-// OTH_OBS_LARGE_REGION bytes of output.  1,048,576 8x8 boards, 64 boards a wave
-// (every layout) against 4 KiB: int64 board 100.0 -> 94.8 us, make_state f32
-// 208.5 -> 183.6 (torch's fill_ of the same tensors: 81.6 / 157.2); regions of
-// 2 / 8 KiB: 108.0 / 102.2 and 183.2 / 197.6 (profiles/r05/l, profiles/r05/m)
+// from OTH_OBS_SMALL_E boards 64 boards a wave; once the output exceeds
+// OTH_OBS_REGION_MIN_BYTES, as many boards per wave (4..64) as fill about
+// OTH_OBS_LARGE_REGION bytes of output.  8x8, graphed, 64 boards a wave against
+// 4-KiB regions (profiles/r05/s/ab_obs_sweep.jsonl): int64 board at 262,144 /
+// 524,288 / 1,048,576 / 2,097,152 boards (139 / 278 / 556 / 1,112 MB) 22.3 /
+// 42.6 / 99.4 / 208.0 us against 23.6 / 50.8 / 94.2 / 187.5; make_state f32
+// (275 / 550 / 1,101 / 2,202 MB) 42.7 / 101.2 / 209.1 / 422.4 against 51.9 /
+// 93.9 / 182.5 / 363.0 (torch's fill_ of the same tensors: 25.2 / 43.3 / 83.0 /
+// 161.4 and 39.6 / 80.3 / 158.2 / 314.4).  Regions of 2 / 8 / 16 KiB and 64
+// boards a wave in strided 4-KiB chunks lost at 1,048,576 (profiles/r05/l, m, s)
+#ifndef OTH_OBS_REGION_MIN_BYTES
+#define OTH_OBS_REGION_MIN_BYTES (384ll << 20)
+#endif
 #ifndef OTH_OBS_LARGE_REGION
 #define OTH_OBS_LARGE_REGION 4096
 #endif
@@ -371,11 +379,12 @@ constexpr int obs_large_bpw() {
 }
 
 // one wave per BPW boards (k_observe_w), vector stores of 4 squares: N*N % 4 == 0
-template <int N, typename T, bool LARGE>
+// BPW0: boards per wave, or 0 for the layout's 4-KiB regions (obs_large_bpw)
+template <int N, typename T, int BPW0>
 void launch_observe_bpw(oth_env* env, int layout, T* o, hipStream_t st) {
     auto go = [&](auto LC) {
         constexpr int LAY = decltype(LC)::value;
-        constexpr int BPW = LARGE ? obs_large_bpw<N, LAY, T>() : 16;
+        constexpr int BPW = BPW0 ? BPW0 : obs_large_bpw<N, LAY, T>();
         const dim3 gw(grid_for(((long long)env->E + BPW - 1) / BPW * 64));
         launch_k((k_observe_w<N, LAY, T, BPW>), gw, dim3(BLOCK), 0, st, env->boards, env->meta, env->legal, env->E,
                  o);
@@ -391,8 +400,11 @@ void launch_observe_bpw(oth_env* env, int layout, T* o, hipStream_t st) {
 template <int N, typename T>
 void launch_observe_w(oth_env* env, int layout, void* out, hipStream_t st) {
     T* o = static_cast<T*>(out);
-    if (env->E < OTH_OBS_SMALL_E) launch_observe_bpw<N, T, false>(env, layout, o, st);
-    else launch_observe_bpw<N, T, true>(env, layout, o, st);
+    const int planes = layout == OTH_OBS_BOARD_LEGAL ? 2 : (layout == OTH_OBS_MAKE_STATE ? 4 : 1);
+    const long long bytes = (long long)env->E * planes * N * N * (long long)sizeof(T);
+    if (env->E < OTH_OBS_SMALL_E) launch_observe_bpw<N, T, 16>(env, layout, o, st);
+    else if (bytes <= OTH_OBS_REGION_MIN_BYTES) launch_observe_bpw<N, T, 64>(env, layout, o, st);
+    else launch_observe_bpw<N, T, 0>(env, layout, o, st);
 }
 
 template <int N>

@@ -644,9 +644,9 @@ def test_observation_kernels_every_layout_and_alignment(torch_cuda, n):
 
 @pytest.mark.parametrize("n,E", [(8, 65536), (8, 262144), (6, 100003), (10, 70000)])
 def test_observation_kernels_at_size(torch_cuda, n, E):
-    """k_observe_w's two wave shapes (16 boards per wave below 262,144 boards,
-    about 4 KiB of output per wave from there) at the configs' sizes and ragged
-    E: int64 BOARD and f32 MAKE_STATE equal the numpy restatement."""
+    """k_observe_w's wave shapes (16 boards per wave below 262,144 boards, 64
+    from there up to 384 MiB of output) at the configs' sizes and ragged E:
+    int64 BOARD and f32 MAKE_STATE equal the numpy restatement."""
     torch = torch_cuda
     env = make_env(torch, E, n, auto=True, seed=8)
     env.step_policy("random", n_plies=n * n // 2 + 1, record=False)
@@ -658,9 +658,9 @@ def test_observation_kernels_at_size(torch_cuda, n, E):
 
 @pytest.mark.parametrize("n,E", [(8, 262147), (6, 300001)])
 def test_observation_large_launches_every_layout_and_dtype(torch_cuda, n, E):
-    """From 262,144 boards k_observe_w takes as many boards per wave as fill
-    about 4 KiB of output (4 for make_state f32, 8 for the int64 board, up to 64
-    for int8): every layout and dtype at ragged E equal the numpy restatement."""
+    """From 262,144 boards k_observe_w takes 64 boards a wave (and 4-KiB output
+    regions past 384 MiB of output: the next test): every layout and dtype at
+    ragged E equal the numpy restatement."""
     torch = torch_cuda
     env = make_env(torch, E, n, auto=True, seed=12)
     env.step_policy("random", n_plies=n * n // 2 + 3, record=False)
@@ -670,6 +670,29 @@ def test_observation_large_launches_every_layout_and_dtype(torch_cuda, n, E):
         for dt in (torch.int8, torch.int32, torch.int64, torch.float32, torch.float64):
             got = env.observe(layout, dt).cpu().numpy()
             np.testing.assert_array_equal(got, want.astype(got.dtype), err_msg="%s %s" % (layout, dt))
+
+
+def test_observation_beyond_384_mib_equals_small_launches(torch_cuda):
+    """Past 384 MiB of output k_observe_w takes as many boards per wave as fill
+    about 4 KiB (make_state f32 and board_legal f64: 4, the int64 board: 8);
+    1,048,579 8x8 boards: slices of each big observation equal the observation
+    of the same boards from a 70,001-board handle (16 boards a wave, itself
+    checked against numpy above)."""
+    torch = torch_cuda
+    E, n = 1048579, 8
+    env = make_env(torch, E, n, auto=True, seed=21)
+    env.step_policy("random", n_plies=37, record=False)
+    b, m, lg = env.get_state()
+    small = make_env(torch, 70001, n, auto=True, seed=21)
+    for lay, dt in (("make_state", torch.float32), ("board", torch.int64), ("board_legal", torch.float64),
+                    ("legal", torch.int8)):
+        big = env.observe(lay, dt)
+        for lo in (0, 500000, E - 70001):
+            small.set_state(b[lo:lo + 70001], m[lo:lo + 70001], lg[lo:lo + 70001])
+            assert torch.equal(big[lo:lo + 70001], small.observe(lay, dt)), "%s %s at %d" % (lay, dt, lo)
+        del big
+    small.close()
+    env.close()
 
 
 @pytest.mark.parametrize("n,opp", [(8, "random"), (6, "greedy")])
