@@ -69,7 +69,8 @@ def state_np(env):
     return b.cpu().numpy().view(np.uint64), m.cpu().numpy().view(np.uint16), lg.cpu().numpy().view(np.uint64)
 
 
-@pytest.mark.parametrize("n,E", [(8, 65536), (8, 70001), (6, 20000), (4, 777), (8, 1), (10, 5000), (7, 3001)])
+@pytest.mark.parametrize("n,E", [(8, 65536), (8, 70001), (6, 20000), (4, 777), (8, 1), (10, 5000), (7, 3001),
+                                 (10, 70001), (12, 1001), (16, 257), (9, 999)])
 def test_step_observe_every_layout_and_dtype(torch_cuda, n, E):
     """step(observe=True) through oth_step_observe (one launch for one-word boards
     with N*N % 4 == 0: k_ply_step_obs; oth_step's kernel + k_observe otherwise)
