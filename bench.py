@@ -634,12 +634,14 @@ def step_observe_lines(E, n, dev, stream, plies=32):
                            "us_per_ply": _r(us["step_board_fused"]),
                            "two_launch_us": _r(us["step_board_split"]),
                            "algorithmic_bytes_per_board": step_b + 8 * NN,
-                           "frac": frac(b_board, us["step_board_fused"])},
+                           "frac": frac(b_board, us["step_board_fused"]),
+                           "pmc": pmc_ref("step-observe-board-int64-%dx%d-E%d" % (n, n, E))},
             "sample_step_make_state": {"kernel": "k_sample_step2<%d> + obs tail" % n,
                                        "us_per_ply": _r(us["sample_step_make_state_fused"]),
                                        "two_launch_us": _r(us["sample_step_make_state_split"]),
                                        "algorithmic_bytes_per_board": 4 * NN + 12 + step_b + 16 * NN,
-                                       "frac": frac(b_ms, us["sample_step_make_state_fused"])},
+                                       "frac": frac(b_ms, us["sample_step_make_state_fused"]),
+                                       "pmc": pmc_ref("sample-step-make-state-f32-%dx%d-E%d" % (n, n, E))},
             "timing": "HIP graph of %d calls from one mid-game state, median of 5 replays" % plies}
 
 
