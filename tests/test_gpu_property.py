@@ -11,7 +11,8 @@ any board), against the oracle restatement on the same positions:
     count_disks (:468-471);
   * GreedyPolicy and MaxiMin-2 / -3 (simple_policies.py:69-163);
   * multi-ply random and greedy play with auto-reset from such positions;
-  * OthelloEnv.step on the device against random and greedy opponents.
+  * OthelloEnv.step on the device against random and greedy opponents;
+  * the single-board record of oth_step_sync and the learners' fused ply.
 
 Hypothesis draws the board size, the disc densities and the seed of the
 position generator (derandomized: the same examples every run, no example
@@ -241,3 +242,74 @@ def test_step_vs_from_arbitrary_positions(torch_cuda, n, seed, db, dw, opp):
     np.testing.assert_array_equal(m, s.meta)
     np.testing.assert_array_equal(lg, s.legal)
     np.testing.assert_array_equal(o.cpu().numpy(), oracle.observe(s)[0].astype(np.int64))
+
+
+@settings(**SETTINGS)
+@given(sd=st.booleans(), which=st.integers(0, E - 1), **position)
+def test_step_sync_record_on_arbitrary_positions(torch_cuda, n, seed, db, dw, sd, which):
+    """oth_step_sync (the drop-in's one launch per step(): the board stepped with
+    a host action, then its whole record written into mapped host memory) on an
+    arbitrary position: state, reward / done, count_disks, GreedyPolicy's move
+    and both observation layouts equal the oracle's."""
+    import ctypes
+
+    from gymothelloenv_amd import _lib as L
+    torch = torch_cuda
+    s = _positions(n, seed, db, min(dw, 1.0 - db))
+    env = _env(n, sd)
+    _load(torch, env, s)
+    one = oracle.State(n, 1)
+    one.boards[:], one.meta[:], one.legal[:] = s.boards[which], s.meta[which], s.legal[which]
+    nn, W = n * n, s.W
+    rng = np.random.RandomState(seed ^ 0x1234)
+    legal = [a for a in range(nn) if (int(one.legal[0, a // 64]) >> (a % 64)) & 1]
+    a = int(rng.choice(legal)) if legal and rng.rand() < 0.7 else int(rng.randint(-2, nn + 2))
+    orw, od, _ = oracle.step(one, oracle.F_SUDDEN_DEATH if sd else 0, np.array([a], dtype=np.int32))
+    layout = L.OTH_OBS_BOARD_LEGAL if seed & 1 else L.OTH_OBS_BOARD
+    ptr = ctypes.c_void_p()
+    L.check(env._lib.oth_step_sync(env._h, which, 1, a, layout, ctypes.byref(ptr), env._stream()), "oth_step_sync")
+    rec = L.OthRecord.from_address(ptr.value)
+    assert list(rec.black)[:W] == list(one.boards[0, :W]) and list(rec.white)[:W] == list(one.boards[0, W:])
+    assert list(rec.legal)[:W] == list(one.legal[0]) and rec.meta == one.meta[0]
+    assert (rec.reward, rec.done) == (int(orw[0]), int(od[0]))
+    wb = oracle.count_disks(one)[0]
+    assert (rec.white_cnt, rec.black_cnt) == (wb[0], wb[1])
+    if not one.meta[0] & 2:
+        now = [x for x in range(nn) if (int(one.legal[0, x // 64]) >> (x % 64)) & 1]
+        assert rec.greedy == (int(oracle.greedy(one)[0]) if now else -1)
+    obs, obs2, _ = oracle.observe(one)
+    got = np.ctypeslib.as_array(rec.obs)[:(2 if seed & 1 else 1) * nn]
+    np.testing.assert_array_equal(got, (obs2 if seed & 1 else obs).reshape(-1))
+
+
+@settings(**SETTINGS)
+@given(lay=st.sampled_from(["board", "board_legal", "make_state"]), **position)
+def test_sample_step_observe_on_arbitrary_positions(torch_cuda, n, seed, db, dw, lay):
+    """The learners' fused ply (oth_sample_step_observe: masked sample, step and
+    the next observation in one launch where the board is one word) from
+    arbitrary positions -- including boards without a possible move (action 0,
+    log-prob 0: model.py:69-71) -- equals sample_actions + step + observe on a
+    twin handle, and the step and observation equal the oracle's."""
+    torch = torch_cuda
+    s = _positions(n, seed, db, min(dw, 1.0 - db))
+    fused = _env(n)
+    twin = _ENVS.setdefault((n, "twin"), None)  # a second handle with the same flags and seed
+    if twin is None:
+        from gymothelloenv_amd import VecOthelloEnv
+        twin = _ENVS[(n, "twin")] = VecOthelloEnv(E, board_size=n, auto_reset=False, seed=0, device="cuda:0")
+    _load(torch, fused, s)
+    _load(torch, twin, s)
+    fused.sample_counter = twin.sample_counter = 0
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    logits = torch.randn(E, n * n, device="cuda", generator=g) * 2
+    a1, lp1, en1, r1, d1, o1 = fused.sample_step(logits, observe=lay, obs_dtype=torch.float32)
+    a2, lp2, en2 = twin.sample_actions(logits)
+    _, r2, d2, _ = twin.step(a2, observe=False)
+    o2 = twin.observe(lay, torch.float32)
+    assert torch.equal(a1, a2) and torch.equal(lp1, lp2) and torch.equal(en1, en2)
+    assert torch.equal(r1, r2) and torch.equal(d1, d2) and torch.equal(o1, o2)
+    orw, od, _ = oracle.step(s, oracle.F_SUDDEN_DEATH, a1.cpu().numpy())
+    np.testing.assert_array_equal(r1.cpu().numpy(), orw)
+    obs, obs2, ms = oracle.observe(s)
+    want = {"board": obs, "board_legal": obs2, "make_state": ms}[lay]
+    np.testing.assert_array_equal(o1.cpu().numpy(), want.astype(np.float32))
