@@ -40,6 +40,8 @@ OTH_GRAPH_COUNTER_SHIFT = 40
 
 OTH_RECORD_MAX_WORDS = 4
 OTH_RECORD_MAX_SQUARES = 256
+OTH_RECORD_GREEDY = 2  # oth_step_sync's `step` bit: the record carries GreedyPolicy's move
+OTH_RECORD_NO_GREEDY = -2
 
 
 class OthRecord(ctypes.Structure):

@@ -282,9 +282,9 @@ int oth_step_sync(oth_env* env, int32_t board, int32_t step, int32_t action, int
         env->rec_seq = 0;
     }
     const uint32_t seq = ++env->rec_seq;
-    const uint64_t ply = step ? env->ply++ : env->ply;
+    const uint64_t ply = (step & 1) ? env->ply++ : env->ply;
     const int rc = with_n(env->n, [&](auto NC) {
-        return launch_record<decltype(NC)::value>(env, board, step ? 1 : 0, action,
+        return launch_record<decltype(NC)::value>(env, board, step & (1 | OTH_RECORD_GREEDY), action,
                                                   layout == OTH_OBS_BOARD_LEGAL ? 2 : 1, ply, (hipStream_t)stream);
     });
     if (rc) return rc;

@@ -25,16 +25,22 @@ NO_DISK = 0
 WHITE_DISK = 1
 
 
+# the set squares of each byte value at each byte offset of a word: possible_moves
+# decoded a byte at a time (half the host time of a bit-by-bit loop; config 1 reads
+# it on every ply)
+_BYTE_SQUARES = [[tuple(8 * k + i for i in range(8) if (b >> i) & 1) for b in range(256)] for k in range(8)]
+
+
 def _mask_to_list(words, nn):
     out = []
     for wi, w in enumerate(words):
-        w = int(w) & 0xFFFFFFFFFFFFFFFF
-        while w:
-            low = w & -w
-            a = 64 * wi + low.bit_length() - 1
-            if a < nn:
-                out.append(a)
-            w ^= low
+        base = 64 * wi
+        for k, b in enumerate((int(w) & 0xFFFFFFFFFFFFFFFF).to_bytes(8, "little")):
+            if b:
+                sq = _BYTE_SQUARES[k][b]
+                out.extend(sq if not base else [base + a for a in sq])
+    if out and out[-1] >= nn:  # (never for a legal mask: it lies on the board)
+        out = [a for a in out if a < nn]
     return out
 
 
@@ -79,6 +85,10 @@ class OthelloBaseEnv(object):
         self._obs_shape = (2, n, n) if possible_actions_in_obs else (n, n)
         self._sync_fn = self._vec._lib.oth_step_sync
         self._recp = ctypes.c_void_p()
+        self._recp_ref = ctypes.byref(self._recp)
+        # the record's GreedyPolicy move costs the call about 0.5 us: asked for once a
+        # GreedyPolicy reads this env (GreedyPolicy.reset / _greedy_move)
+        self._greedy_bit = 0
         self._rec = None  # L.OthRecord over the handle's mapped host record (oth_step_sync)
         self._dirty = True
         # Initialize internal states (othello.py:238-242): no possible moves until reset().
@@ -94,7 +104,7 @@ class OthelloBaseEnv(object):
         """oth_step_sync: (step and) record the board in one launch and one wait;
         the record stays in the handle's mapped host buffer, decoded lazily."""
         v = self._vec
-        rc = self._sync_fn(v._hv, 0, step, action, self._layout, ctypes.byref(self._recp), v._stream())
+        rc = self._sync_fn(v._hv, 0, step | self._greedy_bit, action, self._layout, self._recp_ref, v._stream())
         if rc:
             L.check(rc, "oth_step_sync")
         if self._rec is None or ctypes.addressof(self._rec) != self._recp.value:
@@ -173,6 +183,9 @@ class OthelloBaseEnv(object):
     def _greedy_move(self):
         """GreedyPolicy.get_action for the side to move, from the record (-1: no move)."""
         self._sync()
+        if self._rec.greedy == L.OTH_RECORD_NO_GREEDY:  # first greedy read: records carry it from now on
+            self._greedy_bit = L.OTH_RECORD_GREEDY
+            self._call(0)
         return self._rec.greedy
 
     def _push_meta(self, meta):

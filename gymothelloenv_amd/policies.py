@@ -13,6 +13,7 @@ copied envs.
 """
 import numpy as np
 
+from . import _lib as L
 from .othello import WHITE_DISK
 
 PROTAGONIST_TURN = 1  # simple_policies.py:8-9
@@ -56,6 +57,7 @@ class GreedyPolicy(object):
 
     def reset(self, env):
         self.env = _base(env)
+        self.env._greedy_bit = L.OTH_RECORD_GREEDY  # the env's records carry the greedy move from now on
 
     def get_action(self, obs):
         obs = np.asarray(obs)

@@ -263,6 +263,8 @@ int oth_sample_step_observe(oth_env *env, const float *logits, int64_t ld, const
  * classes (OthelloBaseEnv / SimpleOthelloEnv / OthelloEnv, othello.py:21-501;
  * BASELINE config 1) return it after every call.  W used words per colour. */
 #define OTH_RECORD_MAX_WORDS 4
+#define OTH_RECORD_GREEDY 2       /* oth_step_sync's `step` bit: also compute the record's greedy move */
+#define OTH_RECORD_NO_GREEDY (-2) /* the record's greedy field when that bit was not given */
 #define OTH_RECORD_MAX_SQUARES 256
 typedef struct oth_record {
     uint64_t black[OTH_RECORD_MAX_WORDS]; /* the board (exchange format) */
@@ -275,19 +277,23 @@ typedef struct oth_record {
     int32_t reward;                       /* the step's reward (0 without a step) */
     int32_t white_cnt, black_cnt;         /* count_disks (othello.py:468-471) */
     int32_t greedy;                       /* GreedyPolicy.get_action for the side to move (simple_policies.py:69-92);
-                                             -1 without a possible move */
+                                             -1 without a possible move; OTH_RECORD_NO_GREEDY unless the call
+                                             asked for it (OTH_RECORD_GREEDY) */
     int8_t obs[2 * OTH_RECORD_MAX_SQUARES];   /* get_observation() (othello.py:363-378): planes x N x N */
     int8_t board_state[OTH_RECORD_MAX_SQUARES]; /* board_state (othello.py:257): white +1, black -1 */
 } oth_record;
 
-/* The single-board drop-in path in one launch and one wait: if step != 0,
+/* The single-board drop-in path in one launch and one wait: if step & 1,
  * OthelloBaseEnv.step (othello.py:412-462) of board `board` with the host value
  * `action` (any int: not in possible_moves takes the invalid path; a
  * terminated board is left as it is and reports done, as oth_step), then the
  * board's record (layout OTH_OBS_BOARD or OTH_OBS_BOARD_LEGAL for obs) is
  * written by the same kernel into a mapped host buffer the handle owns, and the
  * call returns once it has landed: *out points at it until the next call on
- * this handle.  step == 0 only records (after reset / set_state / set_player_turn). */
+ * this handle.  step & 1 == 0 only records (after reset / set_state /
+ * set_player_turn).  step & OTH_RECORD_GREEDY also computes GreedyPolicy's move
+ * for the side to move (one lane's bit-plane flip counts: about 0.5 us of the
+ * call, so only when a greedy policy reads the record). */
 int oth_step_sync(oth_env *env, int32_t board, int32_t step, int32_t action, int32_t layout,
                   const oth_record **out, oth_stream_t stream);
 

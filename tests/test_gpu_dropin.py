@@ -176,7 +176,8 @@ def test_maximin_policy_dropin(pkg, golden_dir):
 @pytest.mark.parametrize("n,E,board", [(8, 1, 0), (6, 7, 5), (10, 3, 1), (16, 2, 1), (7, 70, 64)])
 def test_step_sync_record_matches_oracle(pkg, n, E, board):
     """oth_step_sync (the drop-in's one launch per step()): the record of board
-    `board` -- state, reward / done, count_disks, GreedyPolicy's move,
+    `board` -- state, reward / done, count_disks, GreedyPolicy's move (when
+    asked for with OTH_RECORD_GREEDY, else OTH_RECORD_NO_GREEDY),
     get_observation in both layouts, board_state -- equals the oracle after the
     same steps (legal, illegal and out-of-range actions, both sudden-death
     modes); the handle's other boards are untouched."""
@@ -205,8 +206,9 @@ def test_step_sync_record_matches_oracle(pkg, n, E, board):
                 step = 1
                 orw, od, _ = oracle.step(s, flags, np.array([a], dtype=np.int32))
             layout = L.OTH_OBS_BOARD_LEGAL if p % 2 else L.OTH_OBS_BOARD
-            L.check(lib.oth_step_sync(env._h, board, step, a, layout, ctypes.byref(ptr), env._stream()),
-                    "oth_step_sync")
+            want = p % 3 != 0  # the greedy move only when asked for (OTH_RECORD_GREEDY)
+            L.check(lib.oth_step_sync(env._h, board, step | (L.OTH_RECORD_GREEDY if want else 0), a, layout,
+                                      ctypes.byref(ptr), env._stream()), "oth_step_sync")
             rec = L.OthRecord.from_address(ptr.value)
             what = "%dx%d sd=%d ply %d a=%d" % (n, n, sd, p, a)
             assert list(rec.black)[:W] == list(s.boards[0, :W]) and list(rec.white)[:W] == list(s.boards[0, W:]), what
@@ -216,7 +218,9 @@ def test_step_sync_record_matches_oracle(pkg, n, E, board):
                 assert (rec.reward, rec.done) == (int(orw[0]), int(od[0])), what
             wb = oracle.count_disks(s)[0]
             assert (rec.white_cnt, rec.black_cnt) == (wb[0], wb[1]), what
-            if not s.meta[0] & 2:  # (a terminal record's possible_moves are stale: no policy reads them)
+            if not want:
+                assert rec.greedy == L.OTH_RECORD_NO_GREEDY, what
+            elif not s.meta[0] & 2:  # (a terminal record's possible_moves are stale: no policy reads them)
                 now = [x for x in range(nn) if (int(s.legal[0, x // 64]) >> (x % 64)) & 1]
                 assert rec.greedy == (int(oracle.greedy(s)[0]) if now else -1), what
             obs, obs2, _ = oracle.observe(s)

@@ -267,7 +267,8 @@ def test_step_sync_record_on_arbitrary_positions(torch_cuda, n, seed, db, dw, sd
     orw, od, _ = oracle.step(one, oracle.F_SUDDEN_DEATH if sd else 0, np.array([a], dtype=np.int32))
     layout = L.OTH_OBS_BOARD_LEGAL if seed & 1 else L.OTH_OBS_BOARD
     ptr = ctypes.c_void_p()
-    L.check(env._lib.oth_step_sync(env._h, which, 1, a, layout, ctypes.byref(ptr), env._stream()), "oth_step_sync")
+    L.check(env._lib.oth_step_sync(env._h, which, 1 | L.OTH_RECORD_GREEDY, a, layout, ctypes.byref(ptr),
+                                   env._stream()), "oth_step_sync")
     rec = L.OthRecord.from_address(ptr.value)
     assert list(rec.black)[:W] == list(one.boards[0, :W]) and list(rec.white)[:W] == list(one.boards[0, W:])
     assert list(rec.legal)[:W] == list(one.legal[0]) and rec.meta == one.meta[0]
