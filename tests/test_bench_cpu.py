@@ -84,3 +84,14 @@ def test_single_rank_dry_run():
     assert r.returncode == 0, r.stderr[-2000:]
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["shards"] == [[0, 0, 65536]] and d["plies_per_step"] == 100
+
+
+def test_fused_path_pmc_records_are_committed():
+    """The bench's step_observe entries name committed PMC records (traffic per
+    launch within a few percent of the algorithmic bytes: no re-reads)."""
+    import bench
+    for key in ("step-observe-board-int64-8x8-E65536", "sample-step-make-state-f32-8x8-E65536"):
+        rec = bench.load_pmc(key)
+        assert rec and rec["source"].startswith("profiles/")
+        assert 0.95 < rec["hbm_bytes_per_launch"] / rec["algorithmic_bytes_per_launch"] < 1.1
+        assert bench.pmc_ref(key)["hbm_bytes_per_launch"] > 0
