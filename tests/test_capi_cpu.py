@@ -78,6 +78,14 @@ def test_mask_conversions():
         plus, minus = _board_to_masks(board, n)
         assert _mask_to_list(plus.view(np.uint64), n * n) == moves[: n // 2]
         assert _mask_to_list(minus.view(np.uint64), n * n) == moves[n // 2:]
+    # the byte-table decode against a bit-by-bit one on random words, bits past nn dropped
+    rng = np.random.RandomState(5)
+    for W in (1, 2, 4):
+        for _ in range(300):
+            words = rng.randint(-2 ** 63, 2 ** 63 - 1, size=W, dtype=np.int64).view(np.uint64)
+            nn = int(rng.randint(1, 64 * W + 1))
+            want = [a for a in range(64 * W) if (int(words[a // 64]) >> (a % 64)) & 1 and a < nn]
+            assert _mask_to_list(words, nn) == want
 
 
 def test_spaces():
