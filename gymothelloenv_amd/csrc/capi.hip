@@ -124,21 +124,87 @@ __global__ __launch_bounds__(256) void k_reduce_wdl(unsigned long long* __restri
     if (threadIdx.x < 3) out[threadIdx.x] = (int64_t)acc[0][threadIdx.x];
 }
 
+// The leaves of one MaxiMin(d) search from a position with e empty squares:
+// `root` moves at the root, then at most min(b, e - j) at level j, since every
+// level places a disc (simple_policies.py:138) and a full board ends the game
+// (:117-121); b = max(2, N*N / 6) moves per position (8x8 middle games: ~10).
+double search_leaves(int d, int e, double root, double b) {
+    double leaves = 1.0;
+    for (int j = 0; j < d && j < e; ++j) {
+        const double moves = j == 0 ? root : (b < e - j ? b : (double)(e - j));
+        if (moves <= 0.0) break;  // no move: the search stops here (:120)
+        leaves *= moves;
+    }
+    return leaves;
+}
+
+enum MaximinCall { MM_POLICY, MM_STEP_VS, MM_RESET_VS };
+
 // MaxiMin searches of depth >= 3 are refused above OTH_MAXIMIN_LEAF_BUDGET
-// estimated leaves per call: E x b^d x `searches` (the searches one board runs in
-// the call: plies of oth_step_policy, opponent replies of oth_step_vs), with b =
-// max(2, N*N / 6) moves per position (8x8 middle games: ~10)
-int maximin_budget(const oth_env* env, int policy, double searches) {
+// estimated leaves per call.  First E x b^d x `searches` (the searches one board
+// runs in the call: plies of oth_step_policy, opponent replies of the _vs calls);
+// above the budget, the boards are read and each live board's search bounded by
+// its own position (search_leaves: its empty squares, and its possible_moves at
+// the root of a policy call), so late-game boards are searched at any depth the
+// budget allows -- one 8x8 board with 10 empty squares at depth 10 is <= 10!
+// leaves, where the position-blind estimate says 1.9e10.
+int maximin_budget(const oth_env* env, int policy, double searches, MaximinCall call, hipStream_t st) {
     if (policy < OTH_POLICY_MAXIMIN(3) || policy > OTH_POLICY_LAST) return OTH_OK;
-    const int d = policy - OTH_POLICY_MAXIMIN1 + 1;
-    const double b = env->n * env->n / 6.0 > 2.0 ? env->n * env->n / 6.0 : 2.0;
+    const int d = policy - OTH_POLICY_MAXIMIN1 + 1, nn = env->n * env->n;
+    const double b = nn / 6.0 > 2.0 ? nn / 6.0 : 2.0;
     double leaves = (double)env->E * searches;
     for (int i = 0; i < d; ++i) leaves *= b;
     if (leaves <= OTH_MAXIMIN_LEAF_BUDGET) return OTH_OK;
-    char msg[240];
-    snprintf(msg, sizeof(msg), "MaxiMin depth %d over %d boards of %dx%d (x%.0f searches) is ~%.1e leaves, above the "
-             "budget of %.1e per call: split the boards over calls", d, env->E, env->n, env->n, searches, leaves,
-             (double)OTH_MAXIMIN_LEAF_BUDGET);
+    const char* why = "";
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (call == MM_RESET_VS) {
+        why = " (reset_vs searches from the start position)";
+    } else if (hipStreamIsCapturing(st, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) {
+        why = " (during a stream capture the boards cannot be read for a position-aware estimate)";
+    } else {
+        const size_t E = (size_t)env->E, W = (size_t)env->W;
+        uint64_t* bd = new (std::nothrow) uint64_t[E * 3 * W];
+        uint16_t* meta = new (std::nothrow) uint16_t[E];
+        if (!bd || !meta) {
+            delete[] bd;
+            delete[] meta;
+            return fail(OTH_ENOMEM, "maximin budget: host allocation failed");
+        }
+        uint64_t* lg = bd + E * 2 * W;
+        hipError_t err = hipMemcpyAsync(bd, env->boards, E * 2 * W * 8, hipMemcpyDeviceToHost, st);
+        if (err == hipSuccess) err = hipMemcpyAsync(lg, env->legal, E * W * 8, hipMemcpyDeviceToHost, st);
+        if (err == hipSuccess) err = hipMemcpyAsync(meta, env->meta, E * 2, hipMemcpyDeviceToHost, st);
+        if (err == hipSuccess) err = hipStreamSynchronize(st);
+        if (err != hipSuccess) {
+            delete[] bd;
+            delete[] meta;
+            return hip_fail(err, "maximin budget: reading the boards");
+        }
+        // with auto-reset a board that ends is searched again from the start position
+        const bool resets = (env->flags & OTH_AUTO_RESET) != 0;
+        leaves = 0.0;
+        for (size_t i = 0; i < E; ++i) {
+            const bool done = (meta[i] & 2) != 0;
+            if (done && !resets) continue;  // terminated: no search
+            int discs = 0, moves = 0;
+            for (size_t w = 0; w < 2 * W; ++w) discs += __builtin_popcountll(bd[i * 2 * W + w]);
+            for (size_t w = 0; w < W; ++w) moves += __builtin_popcountll(lg[i * W + w]);
+            const int e = nn - discs, later = resets && nn - 4 > e ? nn - 4 : e;
+            const double rest = search_leaves(d, later, b < later ? b : (double)later, b);
+            if (call == MM_POLICY && !done)  // the first search from this position, later plies from <= `later` empties
+                leaves += search_leaves(d, e, (double)moves, b) + (searches - 1.0) * rest;
+            else  // the opponent's replies after the protagonist's move (or searches after a reset)
+                leaves += searches * rest;
+        }
+        delete[] bd;
+        delete[] meta;
+        if (leaves <= OTH_MAXIMIN_LEAF_BUDGET) return OTH_OK;
+        why = " (bounded by each board's empty squares)";
+    }
+    char msg[320];
+    snprintf(msg, sizeof(msg), "MaxiMin depth %d over %d boards of %dx%d (x%.0f searches) is ~%.1e leaves%s, above the "
+             "budget of %.1e per call: split the boards over calls or search shallower", d, env->E, env->n, env->n,
+             searches, leaves, why, (double)OTH_MAXIMIN_LEAF_BUDGET);
     return fail(OTH_EINVAL, msg);
 }
 
@@ -313,7 +379,7 @@ int oth_step_policy(oth_env* env, int32_t policy, int32_t n_plies, int32_t* acti
     if (n_plies < 0) return fail(OTH_EINVAL, "n_plies must be >= 0");
     if (policy < OTH_POLICY_RANDOM || policy > OTH_POLICY_LAST) return fail(OTH_EINVAL, "unknown policy");
     if (n_plies == 0) return OTH_OK;
-    if (int rc = maximin_budget(env, policy, (double)n_plies)) return rc;
+    if (int rc = maximin_budget(env, policy, (double)n_plies, MM_POLICY, (hipStream_t)stream)) return rc;
     const uint64_t ply0 = env->ply;
     env->ply += (uint64_t)n_plies;
     return with_n(env->n, [&](auto NC) {
@@ -327,7 +393,7 @@ int oth_reset_vs(oth_env* env, int32_t opponent_policy, const int8_t* protagonis
     OTH_CHECK_ENV(env);
     if (opponent_policy < OTH_POLICY_RANDOM || opponent_policy > OTH_POLICY_LAST)
         return fail(OTH_EINVAL, "unknown opponent policy");
-    if (int rc = maximin_budget(env, opponent_policy, 2.0)) return rc;
+    if (int rc = maximin_budget(env, opponent_policy, 2.0, MM_RESET_VS, (hipStream_t)stream)) return rc;
     const uint64_t call = env->ply++;
     return with_n(env->n, [&](auto NC) {
         return launch_reset_vs<decltype(NC)::value>(env, opponent_policy, protagonist, mask, call,
@@ -341,7 +407,7 @@ int oth_step_vs(oth_env* env, int32_t opponent_policy, const int32_t* actions, c
     if (!actions) return fail(OTH_EINVAL, "actions is NULL");
     if (opponent_policy < OTH_POLICY_RANDOM || opponent_policy > OTH_POLICY_LAST)
         return fail(OTH_EINVAL, "unknown opponent policy");
-    if (int rc = maximin_budget(env, opponent_policy, 2.0)) return rc;
+    if (int rc = maximin_budget(env, opponent_policy, 2.0, MM_STEP_VS, (hipStream_t)stream)) return rc;
     const uint64_t call = env->ply++;
     return with_n(env->n, [&](auto NC) {
         return launch_step_vs<decltype(NC)::value>(env, opponent_policy, actions, protagonist, rewards, dones,
@@ -358,7 +424,7 @@ int oth_step_vs_observe(oth_env* env, int32_t opponent_policy, const int32_t* ac
         return fail(OTH_EINVAL, "unknown opponent policy");
     if (layout < OTH_OBS_BOARD || layout > OTH_OBS_LEGAL) return fail(OTH_EINVAL, "unknown layout");
     if (dtype < OTH_I8 || dtype > OTH_F64) return fail(OTH_EINVAL, "unknown dtype");
-    if (int rc = maximin_budget(env, opponent_policy, 2.0)) return rc;
+    if (int rc = maximin_budget(env, opponent_policy, 2.0, MM_STEP_VS, (hipStream_t)stream)) return rc;
     const uint64_t call = env->ply++;
     return with_n(env->n, [&](auto NC) {
         return launch_step_vs<decltype(NC)::value>(env, opponent_policy, actions, protagonist, rewards, dones,
@@ -371,7 +437,7 @@ int oth_policy_actions(oth_env* env, int32_t policy, int32_t* out, oth_stream_t 
     if (!out) return fail(OTH_EINVAL, "out is NULL");
     if (policy < OTH_POLICY_GREEDY || policy > OTH_POLICY_LAST)
         return fail(OTH_EINVAL, "policy must be greedy or maximin (depth 1 .. OTH_MAXIMIN_MAX_DEPTH)");
-    if (int rc = maximin_budget(env, policy, 1.0)) return rc;
+    if (int rc = maximin_budget(env, policy, 1.0, MM_POLICY, (hipStream_t)stream)) return rc;
     return with_n(env->n, [&](auto NC) {
         return launch_policy_actions<decltype(NC)::value>(env, policy, out, (hipStream_t)stream);
     });

@@ -12,6 +12,7 @@ control flow around that engine, with the same np.random.RandomState calls
 in the same order, so seeded runs reproduce the reference's trajectories.
 """
 import ctypes
+import operator
 
 import numpy as np
 import torch
@@ -52,6 +53,17 @@ def _list_to_mask(moves, n):
         if 0 <= a < n * n:
             words[a // 64] |= 1 << (a % 64)
     return np.array([w if w < 2 ** 63 else w - 2 ** 64 for w in words], dtype=np.int64)
+
+
+def _square(action):
+    """The square an action names when it is an integer (int, bool, numpy integer,
+    0-d integer tensor: anything with __index__), else None."""
+    if type(action) is int:
+        return action
+    try:
+        return operator.index(action)
+    except TypeError:
+        return None
 
 
 def _board_to_masks(board, n):
@@ -257,14 +269,21 @@ class OthelloBaseEnv(object):
 
     def step(self, action):
         """othello.py:412-462: returns (observation, reward, done, None).  One
-        launch steps the board and writes its record to host memory (oth_step_sync)."""
+        launch steps the board and writes its record to host memory (oth_step_sync).
+
+        Validity is the reference's `action not in self.possible_moves` (:417):
+        an integer (int, numpy integer, bool, 0-d integer tensor) is a square; any
+        other value is compared with the list by ==, so 19.5 or "19" takes the
+        invalid path, while a non-integral member such as 19.0 reaches
+        update_board, whose board indexing raises IndexError (:392-406)."""
         if self._terminated:
             raise ValueError('Game has terminated!')
-        try:
-            a = int(action)
-        except (TypeError, ValueError):
+        a = _square(action)
+        if a is None:
+            if action in self.possible_moves:
+                self._index_error(action)
             a = -1
-        if not -2 ** 31 <= a < 2 ** 31:
+        elif not -2 ** 31 <= a < 2 ** 31:
             a = -1  # outside int32: not in possible_moves either way
         if not self.mute:  # determine_winner's messages need the move's validity
             nn = self._n * self._n
@@ -314,20 +333,48 @@ class OthelloBaseEnv(object):
         state = np.array(state)
         self._set_absolute(state if perspective == WHITE_DISK else -state)
 
-    def update_board(self, action):
-        """othello.py:391-410 as a standalone call: flip and place for the mover
-        without the rest of step() (pass / terminal logic)."""
+    def _index_error(self, action):
+        """update_board with a value that is no integer (othello.py:391-406): the
+        board is negated for a black mover (:395-396), then the first in-board
+        neighbour's board[x][y] raises IndexError before any disc is flipped."""
         self._sync()
-        saved = (self._meta, self._legal.copy())
-        moves = self._possible_moves
-        if action not in moves:
-            # the reference flips whatever rays exist even for an illegal square;
-            # route through a one-move legal list so the kernel applies them
-            self.possible_moves = [action]
-        self._vec.step(torch.tensor([int(action)], dtype=torch.int32), observe=False)
+        if self._player_turn == BLACK_DISK:  # -board_state: the two colours' words swap
+            b, _, _ = self._vec.get_state()
+            W = self._W
+            self._vec.set_state(boards=torch.cat([b[:, W:], b[:, :W]], dim=1))
+            self._dirty = True
+        raise IndexError("only integers, slices (`:`), ellipsis (`...`), numpy.newaxis (`None`) and integer or "
+                         "boolean arrays are valid indices (update_board(%r))" % (action,))
+
+    def update_board(self, action):
+        """othello.py:391-410 as a standalone call: for the side to move, flip
+        every capped ray from the square and put the mover's disc on it --
+        whatever the square held (the reference does not look at it, :407) --
+        without the rest of step() (turn, possible_moves and terminal state are
+        left as they were).  The flips are the step kernel's, on the board loaded
+        live with the square as its one possible move; the square itself is then
+        the mover's alone.  A value that is no integer raises IndexError as in
+        the reference; so does a square off the board (the reference raises
+        there too for action >= N*N, after flipping from the row below the
+        board, and wraps negative squares through numpy's negative indexing:
+        neither is reachable from step())."""
+        a = _square(action)
+        if a is None:
+            self._index_error(action)
+        n = self._n
+        if not 0 <= a < n * n:
+            raise IndexError("update_board: square %d is off the %dx%d board" % (a, n, n))
+        self._sync()
+        meta, legal = self._meta, self._legal.copy()
+        self._vec.set_state(meta=torch.tensor([meta & ~2], dtype=torch.int16),
+                            legal=torch.from_numpy(_list_to_mask([a], n)))
+        self._vec.step(torch.tensor([a], dtype=torch.int32), observe=False)
         b, _, _ = self._vec.get_state()
-        self._vec.set_state(boards=b, meta=torch.tensor([saved[0]], dtype=torch.int16),
-                            legal=torch.from_numpy(saved[1].view(np.int64)))
+        b = b.cpu().numpy().view(np.uint64).copy()
+        other = self._W * ((meta & 1) == 0)  # the opponent's words: white's for a black mover
+        b[0, other + a // 64] &= ~np.uint64(1 << (a % 64))
+        self._vec.set_state(boards=torch.from_numpy(b.view(np.int64)), meta=torch.tensor([meta], dtype=torch.int16),
+                            legal=torch.from_numpy(legal.view(np.int64)))
         self._dirty = True
 
     def set_player_turn(self, turn):

@@ -83,8 +83,10 @@ class MaxiMinPolicy(object):
     empty squares, which it equals (every level places a disc), once the board
     has at most 10 empty squares; earlier in the game such a move raises
     (VecOthelloEnv.policy_actions).  The search is exponential in the depth: about b**depth
-    leaves for b moves per position (8x8 middle games: b ~ 10); the C ABI refuses
-    calls estimated above OTH_MAXIMIN_LEAF_BUDGET leaves (1.7e10), and
+    leaves for b moves per position (8x8 middle games: b ~ 10), fewer late in the
+    game (at most e! for e empty squares).  The C ABI refuses calls estimated
+    above OTH_MAXIMIN_LEAF_BUDGET leaves (1.7e10), bounded by the board's own
+    empty squares, so one 8x8 board searches depth 10 from 10 empty squares on;
     DEEP_WARN_LEAVES bounds what runs without a warning."""
 
     DEEP_WARN_LEAVES = 10 ** 6
@@ -99,8 +101,9 @@ class MaxiMinPolicy(object):
         b = max(2, n * n // 6)  # a typical middle-game move count (8x8: ~10)
         if self.max_search_depth > 0 and b ** self.max_search_depth > self.DEEP_WARN_LEAVES:
             import warnings
-            warnings.warn("MaxiMinPolicy(%d) on %dx%d boards searches ~%.0e leaves per move on one GPU lane; "
-                          "middle-game moves can take seconds to minutes" %
+            warnings.warn("MaxiMinPolicy(%d) on %dx%d boards searches up to ~%.0e leaves per middle-game move "
+                          "(one wave of the GPU per board): such moves can take seconds, or be refused above the "
+                          "C ABI's leaf budget; late-game moves (few empty squares) search far fewer" %
                           (self.max_search_depth, n, n, float(b ** self.max_search_depth)), RuntimeWarning)
 
     def get_action(self, obs):

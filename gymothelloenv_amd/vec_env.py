@@ -167,10 +167,12 @@ class VecOthelloEnv(object):
         r = rewards if rewards is not None else self._i32(self.num_envs)
         d = dones if dones is not None else self._u8(self.num_envs)
         ok = self._okbufs
-        if ok is None or ok[0] is not r or ok[1] is not d:  # caller-given buffers: checked once each
+        # caller-given buffers: checked once each, and again if resize_() / set_() moved or shrank them
+        if ok is None or ok[0] is not r or ok[1] is not d or ok[2] != (r.data_ptr(), d.data_ptr(), r.numel(),
+                                                                      d.numel()):
             self._check_out(r, (torch.int32,), "rewards")
             self._check_out(d, (torch.uint8, torch.bool), "dones")
-            self._okbufs = (r, d)
+            self._okbufs = (r, d, (r.data_ptr(), d.data_ptr(), r.numel(), d.numel()))
         st = _RAW_STREAM(self._dev_index) if _RAW_STREAM is not None else self._stream()
         if observe:
             lay, o = self._obs_out(obs_layout, obs_dtype, obs)
@@ -214,13 +216,13 @@ class VecOthelloEnv(object):
                 raise ValueError("observation dtype must be one of %s" % list(_DTYPES))
             return lay, torch.empty(self._obs_shape(lay), dtype=dtype, device=self.device)
         ok = self._okobs
-        if ok is None or ok[0] is not out or ok[1] != lay:
+        if ok is None or ok[0] is not out or ok[1] != lay or ok[2] != (out.data_ptr(), out.numel(), out.dtype):
             shape = self._obs_shape(lay)
             if out.dtype not in _DTYPES or out.device != self.device or not out.is_contiguous() or \
                     out.numel() != _numel(shape):
                 raise ValueError("obs must be a contiguous tensor of %s elements (shape %s) of one of %s on %s" %
                                  (_numel(shape), shape, list(_DTYPES), self.device))
-            self._okobs = (out, lay)
+            self._okobs = (out, lay, (out.data_ptr(), out.numel(), out.dtype))
         return lay, out
 
     def step_policy(self, policy="random", n_plies=1, actions=None, rewards=None, dones=None, record=True):
@@ -311,9 +313,17 @@ class VecOthelloEnv(object):
         that level either way, :117-126).  Beyond OTH_MAXIMIN_MAX_DEPTH the call
         therefore runs at the largest empty-square count of the batch's live
         boards when that is at most OTH_MAXIMIN_MAX_DEPTH (bit-identical), and
-        raises otherwise."""
+        raises otherwise.  Depth <= 0 searches nothing: the reference's search
+        stops at the root and returns no move (:117-126), so every board gets -1.
+        Calls the C ABI estimates above OTH_MAXIMIN_LEAF_BUDGET leaves (bounded by
+        each board's empty squares) raise OthelloLibError."""
         if isinstance(policy, str) and policy.startswith("maximin") and policy not in _POLICIES:
-            d = int(policy[len("maximin"):])
+            try:
+                d = int(policy[len("maximin"):])
+            except ValueError:
+                raise ValueError("unknown policy %r: 'greedy' or 'maximin<depth>'" % (policy,)) from None
+            if d <= 0:
+                return torch.full((self.num_envs,), -1, dtype=torch.int32, device=self.device)
             # (a terminated board's search returns no move at the root, whatever the depth)
             live = ~self.terminated()
             left = self.board_size ** 2 - self.count_disks().sum(1)
@@ -323,6 +333,8 @@ class VecOthelloEnv(object):
                                  "%d, or any depth once every board has at most %d empty squares"
                                  % (d, empties, L.OTH_MAXIMIN_MAX_DEPTH, L.OTH_MAXIMIN_MAX_DEPTH))
             policy = "maximin%d" % max(1, min(d, empties))
+        if isinstance(policy, str) and policy not in _POLICIES:
+            raise ValueError("unknown policy %r: 'greedy' or 'maximin<depth>'" % (policy,))
         out = self._i32(self.num_envs)
         L.check(self._lib.oth_policy_actions(self._h, _POLICIES[policy], _ptr(out), self._stream()),
                 "oth_policy_actions")

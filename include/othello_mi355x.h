@@ -68,10 +68,17 @@ enum {
 #define OTH_POLICY_MAXIMIN(d) (OTH_POLICY_MAXIMIN1 + (d) - 1)
 #define OTH_POLICY_LAST OTH_POLICY_MAXIMIN(OTH_MAXIMIN_MAX_DEPTH)
 /* oth_policy_actions, oth_step_policy and oth_reset_vs / oth_step_vs refuse
- * MaxiMin(d >= 3) calls whose searches are estimated above this many leaves:
- * E x b^d x the searches per board in the call (n_plies for oth_step_policy, 2
- * opponent replies for the _vs calls) with b = max(2, N*N / 6) moves per
- * position (8x8 middle games: ~10); split the boards over several calls */
+ * MaxiMin(d >= 3) calls whose searches are estimated above this many leaves.
+ * The first estimate is E x b^d x the searches per board in the call (n_plies
+ * for oth_step_policy, 2 opponent replies for the _vs calls) with b = max(2,
+ * N*N / 6) moves per position (8x8 middle games: ~10).  Above the budget the
+ * call reads the boards (a synchronisation of `stream`; refused during a stream
+ * capture) and bounds each live board's search by its own position: its
+ * possible_moves at the root, then at most min(b, e - j) moves at level j for
+ * e empty squares, since every level places a disc (simple_policies.py:138).
+ * So late-game boards search to any depth the budget allows (one 8x8 board
+ * with 10 empty squares at depth 10: <= 10! leaves).  Refused calls launch
+ * nothing; split the boards over several calls or search shallower. */
 #define OTH_MAXIMIN_LEAF_BUDGET 17179869184.0
 
 /* observation layouts */
@@ -183,7 +190,8 @@ int oth_greedy_actions(oth_env *env, int32_t *out, oth_stream_t stream);
  * for the side to move in every env; -1 where possible_moves is empty.
  * MaxiMin(d >= 3) searches each board with a whole wave (the root's moves and
  * their replies spread over the lanes); above OTH_MAXIMIN_LEAF_BUDGET estimated
- * leaves the call is refused (OTH_EINVAL) before anything is launched. */
+ * leaves (position-aware, see there) the call is refused (OTH_EINVAL) before
+ * anything is launched. */
 int oth_policy_actions(oth_env *env, int32_t policy, int32_t *out, oth_stream_t stream);
 
 /* Observations: layout OTH_OBS_*, dtype OTH_I8..OTH_F64, out (E, planes, N, N). */

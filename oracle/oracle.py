@@ -42,6 +42,7 @@ def lib():
         L.oracle_nwords.argtypes = [i32]
         L.oracle_reset_batch.argtypes = [i32, i32, P, P, P]
         L.oracle_legal_batch.argtypes = [i32, i32, P, P, P]
+        L.oracle_update_board_batch.argtypes = [i32, i32, P, P, P]
         L.oracle_step_batch.argtypes = [i32, u32, u64, u32, u64, i32, i32, P, P, P, P, P, P, P]
         L.oracle_step_batch.restype = i32
         L.oracle_reset_openings.argtypes = [i32, i32, u64, u32, u64, i32, P, P, P]
@@ -119,6 +120,14 @@ def legal(n, mover, opp):
     out = np.zeros((E, nwords(n)), dtype=np.uint64)
     lib().oracle_legal_batch(n, E, _p(mover), _p(opp), _p(out))
     return out
+
+
+def update_board(s, actions):
+    """update_board (othello.py:391-410) alone, in place on s.boards: the side to
+    move flips from square actions[i] (any square of the board, occupied or not)
+    and puts its disc there; meta and legal are untouched."""
+    actions = np.ascontiguousarray(actions, dtype=np.int32)
+    lib().oracle_update_board_batch(s.n, s.E, _p(s.boards), _p(s.meta), _p(actions))
 
 
 def step(s, flags, actions, seed=0, id_base=0, ply=0, initial_rand_steps=0, wdl=None):

@@ -319,6 +319,24 @@ void oracle_legal_batch(int n, int E, const uint64_t *mover, const uint64_t *opp
     }
 }
 
+/* update_board (othello.py:391-410) alone for E envs: the side to move (meta
+ * bit 0) flips every capped ray from square actions[i] in [0, N*N) and puts its
+ * disc on it, whatever the square held; meta and possible_moves are untouched
+ * (only boards is written). */
+void oracle_update_board_batch(int n, int E, uint64_t *boards, const uint16_t *meta, const int32_t *actions) {
+    int W = nwords(n);
+    uint64_t lg[MAXW], lg_out[MAXW];
+    uint16_t m_out;
+    memset(lg, 0, sizeof(lg));
+    oenv e;
+    for (int i = 0; i < E; i++) {
+        memset(&e, 0, sizeof(e));
+        load(&e, n, 0, boards + (size_t)i * 2 * W, meta[i], lg);
+        update_board(&e, actions[i]);
+        store(&e, boards + (size_t)i * 2 * W, &m_out, lg_out);
+    }
+}
+
 /* OthelloBaseEnv.step (othello.py:412-462) for E envs with external actions.
  * A terminated env is left unchanged and reports done=1, reward=0 (the batched
  * stand-in for the reference's ValueError); with F_AUTO_RESET an env that

@@ -13,6 +13,8 @@ colour.
 
     python tests/golden/gen_golden.py        # rewrites tests/golden/*.npz|json
     python tests/golden/gen_golden.py masked # only masked.npz (learners' policy heads)
+    python tests/golden/gen_golden.py edges  # only edges.npz (the drop-in boundary's edges)
+    python tests/golden/gen_golden.py maximin_late  # only maximin_late.npz (depth 10, ~8 min on 6 cores)
 """
 import contextlib
 import io
@@ -490,6 +492,177 @@ def gen_maximin_deeper(othello, simple_policies):
     np.savez_compressed(os.path.join(OUT, "maximin_deeper.npz"), **out)
 
 
+def gen_edges(othello, simple_policies):
+    """The drop-in boundary's edges, from the reference itself (edges.npz):
+      * update_board (othello.py:391-410) called alone on every kind of square --
+        the mover's own disc, the opponent's disc, an empty legal and an empty
+        illegal square -- on positions from random play, N = 6, 8, 10; the
+        board after the call (turn and possible_moves are untouched);
+      * step() with values that are no int (othello.py:417's `in
+        possible_moves` test): a non-member float (x.5), a float / np.float64 /
+        np.float32 equal to a member, a string naming a member, a float equal to
+        a non-member square; the outcome ("ok" with reward and done, or the
+        exception's class name) and the board, turn and possible_moves after it;
+      * MaxiMinPolicy(10) and (12) on late 8x8 positions (<= 6 empty squares)."""
+    out = {}
+    for n in (6, 8, 10):
+        rnd = np.random.RandomState(700 + n)
+        env = othello.OthelloBaseEnv(board_size=n, mute=True)
+        pre_b, pre_w, turns, acts, post_b, post_w = [], [], [], [], [], []
+        while len(acts) < 240:
+            env.reset()
+            done = False
+            while not done:
+                if rnd.rand() < 0.35:
+                    flat = np.asarray(env.board_state).ravel()
+                    me = env.player_turn
+                    kinds = [np.flatnonzero(flat == me), np.flatnonzero(flat == -me),
+                             np.array(env.possible_moves, dtype=int),
+                             np.setdiff1d(np.flatnonzero(flat == 0), env.possible_moves)]
+                    for sq in kinds:
+                        if len(sq) == 0:
+                            continue
+                        a = int(sq[rnd.randint(0, len(sq))])
+                        probe = othello.OthelloBaseEnv(board_size=n, mute=True)
+                        probe.reset()
+                        probe.board_state = np.array(env.board_state)
+                        probe.player_turn = me
+                        b, w, t, _ = snapshot(probe, n)
+                        probe.update_board(a)
+                        pb, pw = board_bits(probe.board_state, n)
+                        pre_b.append(b)
+                        pre_w.append(w)
+                        turns.append(t)
+                        acts.append(a)
+                        post_b.append(pb)
+                        post_w.append(pw)
+                pm = env.possible_moves
+                _, _, done, _ = env.step(int(pm[rnd.randint(0, len(pm))]))
+        key = "ub_N%d_" % n
+        out[key + "black"] = np.array(pre_b, dtype=np.uint64)
+        out[key + "white"] = np.array(pre_w, dtype=np.uint64)
+        out[key + "turn"] = np.array(turns, dtype=np.int8)
+        out[key + "action"] = np.array(acts, dtype=np.int32)
+        out[key + "post_black"] = np.array(post_b, dtype=np.uint64)
+        out[key + "post_white"] = np.array(post_w, dtype=np.uint64)
+        print("update_board N=%d: %d calls" % (n, len(acts)), flush=True)
+    # step() with values that are no int, from positions of random play (8x8, both colours to move)
+    kinds = ["half", "float_member", "np_float64_member", "np_float32_member", "str_member", "float_nonmember"]
+    rows = {k: [] for k in ("kind", "value", "sudden", "black", "white", "turn", "legal", "outcome", "reward",
+                            "done", "post_black", "post_white", "post_turn", "post_legal")}
+    rnd = np.random.RandomState(811)
+    for sudden in (True, False):
+        for trial in range(24):
+            env = othello.OthelloBaseEnv(board_size=8, mute=True, sudden_death_on_invalid_move=sudden)
+            env.reset()
+            for _ in range(rnd.randint(0, 30)):
+                pm = env.possible_moves
+                _, _, done, _ = env.step(int(pm[rnd.randint(0, len(pm))]))
+                if done:
+                    env.reset()
+            pm = env.possible_moves
+            member = int(pm[rnd.randint(0, len(pm))])
+            empty = np.setdiff1d(np.flatnonzero(np.asarray(env.board_state).ravel() == 0), pm)
+            nonmember = int(empty[rnd.randint(0, len(empty))]) if len(empty) else 64
+            values = {"half": member + 0.5, "float_member": float(member),
+                      "np_float64_member": np.float64(member), "np_float32_member": np.float32(member),
+                      "str_member": str(member), "float_nonmember": float(nonmember)}
+            for k in kinds:
+                e2 = othello.OthelloBaseEnv(board_size=8, mute=True, sudden_death_on_invalid_move=sudden)
+                e2.reset()
+                e2.board_state = np.array(env.board_state)
+                e2.set_player_turn(env.player_turn)
+                b, w, t, lg = snapshot(e2, 8)
+                try:
+                    _, r, d, _ = e2.step(values[k])
+                    outcome, r, d = "ok", int(r), int(bool(d))
+                except Exception as ex:  # the reference's own exception (IndexError for a float member)
+                    outcome, r, d = type(ex).__name__, 0, 0
+                pb, pw, pt, plg = snapshot(e2, 8)
+                for name, v in (("kind", kinds.index(k)), ("value", float(values[k])), ("sudden", int(sudden)), ("black", b[0]), ("white", w[0]),
+                                ("turn", t), ("legal", lg[0]), ("outcome", outcome), ("reward", r), ("done", d),
+                                ("post_black", pb[0]), ("post_white", pw[0]), ("post_turn", pt),
+                                ("post_legal", plg[0])):
+                    rows[name].append(v)
+    for name, v in rows.items():
+        dt = {"outcome": "U16", "kind": np.int8, "sudden": np.int8, "turn": np.int8, "post_turn": np.int8,
+              "reward": np.int32, "done": np.int8, "value": np.float64}.get(name, np.uint64)
+        out["st_" + name] = np.array(v, dtype=dt)
+    out["st_kinds"] = np.array(kinds, dtype="U20")
+    print("step with non-int values: %d calls, outcomes %s" % (len(rows["kind"]), sorted(set(rows["outcome"]))),
+          flush=True)
+    # MaxiMinPolicy(10) / (12) on late 8x8 positions
+    for depth in (10, 12):
+        rnd = np.random.RandomState(900 + depth)
+        env = othello.OthelloBaseEnv(board_size=8, mute=True)
+        pol = simple_policies.MaxiMinPolicy(depth)
+        pol.reset(env)
+        blacks, whites, turns, acts = [], [], [], []
+        while len(acts) < 8:
+            env.reset()
+            done = False
+            while not done and len(acts) < 8:
+                empty = 64 - int(np.count_nonzero(env.board_state))
+                if 3 <= empty <= 6 and rnd.rand() < 0.5:
+                    a = pol.get_action(env.get_observation())
+                    b, w, t, _ = snapshot(env, 8)
+                    blacks.append(b)
+                    whites.append(w)
+                    turns.append(t)
+                    acts.append(-1 if a is None else int(a))
+                pm = env.possible_moves
+                _, _, done, _ = env.step(int(pm[rnd.randint(0, len(pm))]))
+        key = "mm_d%d_" % depth
+        out[key + "black"] = np.array(blacks, dtype=np.uint64)
+        out[key + "white"] = np.array(whites, dtype=np.uint64)
+        out[key + "turn"] = np.array(turns, dtype=np.int8)
+        out[key + "action"] = np.array(acts, dtype=np.int32)
+        print("maximin 8x8 depth=%d: %d late positions" % (depth, len(acts)), flush=True)
+    np.savez_compressed(os.path.join(OUT, "edges.npz"), **out)
+
+
+def _maximin_late_task(args):
+    """One MaxiMinPolicy(depth) call on the 8x8 position a seeded random game
+    reaches with exactly `empty` empty squares (a worker process)."""
+    empty_target, depth, seed = args
+    install_shims()
+    import othello  # noqa: E402  (reference, read-only)
+    import simple_policies  # noqa: E402
+    rnd = np.random.RandomState(seed)
+    while True:
+        env = othello.OthelloBaseEnv(board_size=8, mute=True)
+        env.reset()
+        done = False
+        while not done:
+            empty = 64 - int(np.count_nonzero(env.board_state))
+            if empty == empty_target and env.possible_moves:
+                pol = simple_policies.MaxiMinPolicy(depth)
+                pol.reset(env)
+                a = pol.get_action(env.get_observation())
+                b, w, t, _ = snapshot(env, 8)
+                return int(b[0]), int(w[0]), t, -1 if a is None else int(a)
+            pm = env.possible_moves
+            _, _, done, _ = env.step(int(pm[rnd.randint(0, len(pm))]))
+
+
+def gen_maximin_late():
+    """MaxiMinPolicy(10) on 8x8 positions with 7-10 empty squares
+    (maximin_late.npz): the reference's search takes ~2 s at 7 empty squares and
+    ~7 minutes at 10, so the positions run in parallel worker processes."""
+    import multiprocessing
+    tasks = [(e, 10, 4000 + 10 * e + k) for e in (7, 8, 9, 10) for k in range(2)]
+    with multiprocessing.get_context("spawn").Pool(min(len(tasks), 6)) as pool:
+        res = pool.map(_maximin_late_task, tasks, chunksize=1)
+    out = {"mm_late_black": np.array([r[0] for r in res], dtype=np.uint64),
+           "mm_late_white": np.array([r[1] for r in res], dtype=np.uint64),
+           "mm_late_turn": np.array([r[2] for r in res], dtype=np.int8),
+           "mm_late_action": np.array([r[3] for r in res], dtype=np.int32),
+           "mm_late_empty": np.array([t[0] for t in tasks], dtype=np.int32),
+           "mm_late_depth": np.array([t[1] for t in tasks], dtype=np.int32)}
+    print("maximin 8x8 depth 10 at 7-10 empty squares: %d positions" % len(res), flush=True)
+    np.savez_compressed(os.path.join(OUT, "maximin_late.npz"), **out)
+
+
 def install_learner_shims():
     """Stand-ins for what the learners' modules import but the policy heads never
     use: torch.utils.tensorboard (ppo.py:7; tensorboard is absent), the
@@ -630,6 +803,12 @@ def main():
     if sys.argv[1:] == ["maximin_deeper"]:
         gen_maximin_deeper(othello, simple_policies)
         return
+    if sys.argv[1:] == ["edges"]:
+        gen_edges(othello, simple_policies)
+        return
+    if sys.argv[1:] == ["maximin_late"]:
+        gen_maximin_late()
+        return
     gen_kat(othello)
     gen_trajectories(othello)
     gen_greedy(othello, simple_policies, util)
@@ -639,6 +818,8 @@ def main():
     gen_maximin(othello, simple_policies)
     gen_maximin_deep(othello, simple_policies)
     gen_maximin_deeper(othello, simple_policies)
+    gen_edges(othello, simple_policies)
+    gen_maximin_late()
     gen_masked(othello)
 
 

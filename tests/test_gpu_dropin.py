@@ -238,26 +238,35 @@ def test_step_sync_record_matches_oracle(pkg, n, E, board):
 
 
 def test_dropin_step_is_one_launch_per_call(pkg):
-    """The drop-in's step() costs one oth_step_sync call (no state copies, no
-    observe launches, no torch synchronisation): wall time per step well under
-    the 160-200 us of the round-4 path on a warm box, and a GreedyPolicy move
-    costs no device call at all (read from the record)."""
-    import time
+    """The drop-in's step() is exactly one oth_step_sync call (no state copies,
+    no observe launches, no other C-ABI call), and a GreedyPolicy move and the
+    attribute reads after a step cost no device call at all (read from the
+    record).  Counted structurally through a wrapped entry point, not timed (the
+    time per call is a bench figure: bench.py configs.config1_single_board)."""
     env = pkg.OthelloBaseEnv(board_size=8, mute=True)
     pol = pkg.GreedyPolicy()
     pol.reset(env)
     rnd = np.random.RandomState(0)
     env.reset()
-    for _ in range(50):  # warm-up
-        if env.terminated:
-            env.reset()
-        env.step(pol.get_action(env.get_observation()))
-    t0, k = time.perf_counter(), 0
-    while time.perf_counter() - t0 < 0.5:
-        if env.terminated:
-            env.reset()
+    calls = []
+    real = env._sync_fn
+
+    def counted(*a):
+        calls.append(a[2] & 1)  # the `step` bit
+        return real(*a)
+
+    def forbidden(*a, **k):
+        raise AssertionError("a drop-in step() used another device path")
+
+    env._sync_fn = counted
+    env._vec.get_state = env._vec.set_state = env._vec.observe = env._vec.step = forbidden
+    plies = 0
+    while not env.terminated:  # one whole game
+        n0 = len(calls)
         moves = env.possible_moves
-        env.step(moves[rnd.randint(0, len(moves))])
-        k += 1
-    us = (time.perf_counter() - t0) / k * 1e6
-    assert us < 100, "%.1f us per drop-in step" % us
+        a = pol.get_action(env.get_observation()) if plies % 2 else moves[rnd.randint(0, len(moves))]
+        env.step(a)
+        _ = (env.player_turn, env.possible_moves, env.board_state, env.count_disks(), env.winner)
+        assert calls[n0:] == [1], "step() made %r oth_step_sync calls" % (calls[n0:],)
+        plies += 1
+    assert plies > 20

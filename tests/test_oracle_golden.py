@@ -269,3 +269,43 @@ def test_host_make_state_matches_reference(golden_dir, n):
         back = undo_state(st, int(turn[i]))
         np.testing.assert_array_equal(back, obs[i])
     assert singles > 0  # the >= 2 quirk is exercised
+
+
+@pytest.mark.parametrize("n", [6, 8, 10])
+def test_update_board_matches_reference(golden_dir, n):
+    """update_board (othello.py:391-410) alone on the mover's disc, the
+    opponent's disc, empty legal and empty illegal squares (edges.npz): the
+    oracle's board after the call equals the reference's."""
+    g = np.load(os.path.join(golden_dir, "edges.npz"))
+    k = "ub_N%d_" % n
+    W = oracle.nwords(n)
+    a = g[k + "action"]
+    s = oracle.State(n, len(a))
+    s.boards[:] = np.concatenate([g[k + "black"].reshape(-1, W), g[k + "white"].reshape(-1, W)], axis=1)
+    s.meta[:] = oracle.meta_from(g[k + "turn"])
+    oracle.update_board(s, a)
+    want = np.concatenate([g[k + "post_black"].reshape(-1, W), g[k + "post_white"].reshape(-1, W)], axis=1)
+    np.testing.assert_array_equal(s.boards, want)
+
+
+def test_maximin_depth10_late_matches_reference(golden_dir):
+    """MaxiMinPolicy(10) and (12) on late 8x8 positions (edges.npz: 3-6 empty
+    squares; maximin_late.npz: depth 10 at 7-10) -- the positions the C ABI's
+    position-aware leaf budget admits on one board."""
+    g = np.load(os.path.join(golden_dir, "edges.npz"))
+    for depth in (10, 12):
+        k = "mm_d%d_" % depth
+        s = oracle.State(8, len(g[k + "action"]))
+        s.boards[:] = np.concatenate([g[k + "black"], g[k + "white"]], axis=1)
+        s.meta[:] = oracle.meta_from(g[k + "turn"])
+        s.legal[:] = oracle.recompute_legal(s)
+        np.testing.assert_array_equal(oracle.maximin(s, depth), g[k + "action"])
+    late = os.path.join(golden_dir, "maximin_late.npz")
+    if not os.path.exists(late):
+        pytest.skip("maximin_late.npz not generated")
+    z = np.load(late)
+    s = oracle.State(8, len(z["mm_late_action"]))
+    s.boards[:, 0], s.boards[:, 1] = z["mm_late_black"], z["mm_late_white"]
+    s.meta[:] = oracle.meta_from(z["mm_late_turn"])
+    s.legal[:] = oracle.recompute_legal(s)
+    np.testing.assert_array_equal(oracle.maximin(s, 10), z["mm_late_action"])
