@@ -258,6 +258,23 @@ OTH_HD uint64_t sh(uint64_t x) {
     else return x >> -S;
 }
 OTH_HD bool any(uint64_t a) { return a != 0ull; }
+// sh<S> of a plain word whose halves feed 3-input dword ops: kept ONE v_lshl*_b64
+// for |S| < 32 (the backend would split it into v_lshlrev_b32 + v_alignbit_b32, as
+// for U2's sh); |S| >= 32 is a dword move
+template <int S>
+OTH_HD uint64_t sh64(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (S != 0 && S > -32 && S < 32) {
+        if (!__builtin_constant_p(x)) {
+            uint64_t r;
+            if constexpr (S > 0) asm("v_lshlrev_b64 %0, %2, %1" : "=v"(r) : "v"(x), "n"(S));
+            else asm("v_lshrrev_b64 %0, %2, %1" : "=v"(r) : "v"(x), "n"(-S));
+            return r;
+        }
+    }
+#endif
+    return sh<S>(x);
+}
 
 // a ^ b ^ c and majority(a, b, c): symmetric, so the builtin's operand order does not matter
 OTH_HD uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) {
@@ -295,6 +312,26 @@ OTH_HD uint64_t maj3_64(uint64_t a, uint64_t b, uint64_t c) {
     return ((uint64_t)hi << 32) | lo;
 #else
     return (a & b) | (c & (a | b));
+#endif
+}
+// c ? x : y bit by bit: one 3-input op per dword
+OTH_HD uint64_t sel_64(uint64_t c, uint64_t x, uint64_t y) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)c, (uint32_t)x, (uint32_t)y, 0xCA);
+    const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(c >> 32), (uint32_t)(x >> 32), (uint32_t)(y >> 32), 0xCA);
+    return ((uint64_t)hi << 32) | lo;
+#else
+    return (c & x) | (~c & y);
+#endif
+}
+// a | b | c: one 3-input op per dword
+OTH_HD uint64_t or3_64(uint64_t a, uint64_t b, uint64_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, 0xFE);
+    const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), 0xFE);
+    return ((uint64_t)hi << 32) | lo;
+#else
+    return a | b | c;
 #endif
 }
 
@@ -891,25 +928,6 @@ struct OneWord {
         return u64(L & ~(P | O) & u2(BD));
     }
 
-    // Run length along one ray direction (step S) for every square, as a
-    // 3-bit number on bit planes: A_j = {a : a + S, ..., a + jS all in T}
-    // from doubling shifts; the nested A_1..A_6 count in binary as
-    // (A1^..^A6, (A2^A4)|A6, A4).  No wrap-around masks: the horizontal and
-    // diagonal fills hold no edge-column square, and every A_j lies in A_1.
-    template <int S>
-    static OTH_HD void run_len(uint64_t T, uint64_t out[3]) {
-        constexpr int R = N - 2;
-        const uint64_t A1 = sh<-S>(T);
-        uint64_t A2 = 0, A3 = 0, A4 = 0, A5 = 0, A6 = 0;
-        if constexpr (R >= 2) A2 = A1 & sh<-S>(A1);
-        if constexpr (R >= 3) A3 = A2 & sh<-2 * S>(A1);
-        if constexpr (R >= 4) A4 = A2 & sh<-2 * S>(A2);
-        if constexpr (R >= 5) A5 = A4 & sh<-4 * S>(A1);
-        if constexpr (R >= 6) A6 = A4 & sh<-4 * S>(A2);
-        out[0] = xor3_64(xor3_64(A1, A2, A3), A4, A5) ^ A6;
-        out[1] = (A2 ^ A4) | A6;
-        out[2] = A4;
-    }
     // out[0..NO) = a[0..NA) + b[0..NB) on bit planes (ripple carry, carries past NO
     // dropped): a half adder, then one 3-input op per dword for each sum and carry
     template <int NA, int NB, int NO>
@@ -927,6 +945,59 @@ struct OneWord {
             }
         }
     }
+    // The run length of every square along ray direction S -- how many of
+    // a + S, a + 2S, ... lie in T before the first that does not (at most N - 2
+    // for a fill) -- in binary (out[2], out[1], out[0]), by doubling a window:
+    // L2 = min(r, 2) from T at a + S and a + 2S, L4 = L2 + [L2 = 2] L2(a + 2S),
+    // L8 = L4 + [L4 = 4] L4(a + 4S): 6 shifts and 7 two- or three-input ops per
+    // dword (20 VALU at 8x8, against 24 for the nested thermometer A_j =
+    // {a : a + S, ..., a + jS all in T}, j = 1..6, and its binary code).  A
+    // window is read past the square only when every square before it lies in
+    // T; a horizontal or diagonal fill holds no edge-column square, so no
+    // window that counts reads across a row's end.
+    template <int S>
+    static OTH_HD void run_bin(uint64_t T, uint64_t out[3]) {
+        constexpr int R = N - 2;
+        static_assert(R >= 2 && R <= 6, "N = 4 .. 8");
+        const uint64_t x1 = sh64<-S>(T), y = sh64<-S>(x1);
+        const uint64_t b1 = x1 & y, b0 = x1 & ~y;  // L2 = 2 b1 + b0
+        if constexpr (R == 2) {
+            out[0] = b0;
+            out[1] = b1;
+            out[2] = 0;
+            return;
+        }
+        const uint64_t b1s = sh64<-2 * S>(b1), b0s = sh64<-2 * S>(b0);
+        const uint64_t c2 = b1 & b1s, c1 = b1 & ~b1s, c0 = sel_64(b1, b0s, b0);  // L4
+        if constexpr (R <= 4) {
+            out[0] = c0;
+            out[1] = c1;
+            out[2] = c2;
+            return;
+        }
+        const uint64_t c1s = sh64<-4 * S>(c1), c0s = sh64<-4 * S>(c0);
+        out[0] = sel_64(c2, c0s, c0);  // L8 (a window of 8 would be a run past the board: never used)
+        out[1] = sel_64(c2, c1s, c1);
+        out[2] = c2;
+    }
+    // tot[0..5) = a[0] + a[1] + a[2] + a[3] for four 3-bit numbers on bit planes
+    // (carry-save: full adders column by column, 18 three-input ops per dword
+    // against 20 for the adder tree add_planes builds)
+    static OTH_HD void sum4_planes(const uint64_t a[4][3], uint64_t tot[5]) {
+        const uint64_t p = xor3_64(a[0][0], a[1][0], a[2][0]), cA = maj3_64(a[0][0], a[1][0], a[2][0]);
+        tot[0] = p ^ a[3][0];
+        const uint64_t cB = p & a[3][0];
+        const uint64_t q1 = xor3_64(a[0][1], a[1][1], a[2][1]), cC = maj3_64(a[0][1], a[1][1], a[2][1]);
+        const uint64_t q2 = xor3_64(a[3][1], cA, cB), cD = maj3_64(a[3][1], cA, cB);
+        tot[1] = q1 ^ q2;
+        const uint64_t cE = q1 & q2;
+        const uint64_t r1 = xor3_64(a[0][2], a[1][2], a[2][2]), cF = maj3_64(a[0][2], a[1][2], a[2][2]);
+        const uint64_t r2 = xor3_64(a[3][2], cC, cD), cG = maj3_64(a[3][2], cC, cD);
+        tot[2] = xor3_64(r1, r2, cE);
+        const uint64_t cH = maj3_64(r1, r2, cE);
+        tot[3] = xor3_64(cF, cG, cH);
+        tot[4] = maj3_64(cF, cG, cH);
+    }
     // GreedyPolicy.get_action (simple_policies.py:69-92): the candidate (a
     // square of `legal`) flipping the most discs, the lowest of equal counts
     // (np.argmax); -1 without candidates.  The eight run lengths are summed on
@@ -934,27 +1005,29 @@ struct OneWord {
     // largest total among the candidates is found plane by plane from the top.
     // Opposite directions are added first: both runs lie on one line through
     // the square, between two own discs, so their sum is at most N - 2 <= 6 and
-    // stays 3 bits (no carry out of the first adders).
+    // stays 3 bits (no carry out of the first adders); the four axis sums meet
+    // in sum4_planes.  Round 6: 331 -> 264 VALU for this function in k_play_rand
+    // <8, GREEDY> (run_bin's doubling instead of the nested thermometer
+    // A_1..A_6, the carry-save sum); config 3, 65,536 boards, 100-ply launches
+    // 1.458 -> 1.377 us per ply on one box (profiles/r06/a).
     // The planes are plain 64-bit words: on dword pairs (U2) the gfx950 backend
     // miscompiled them inside k_play ("A compiler hazard";
     // tests/test_gpu_hazards.py pins the position).
     static OTH_HD int greedy(const uint64_t t[8], uint64_t legal) {
-        uint64_t n[8][3];
-        run_len<1>(t[0], n[0]);
-        run_len<N>(t[1], n[1]);
-        run_len<N + 1>(t[2], n[2]);
-        run_len<N - 1>(t[3], n[3]);
-        run_len<-1>(t[4], n[4]);
-        run_len<-N>(t[5], n[5]);
-        run_len<-N - 1>(t[6], n[6]);
-        run_len<-N + 1>(t[7], n[7]);
         static_assert(N - 2 <= 7, "an axis' two runs fit 3 bits");
-        uint64_t s3[4][3], s4[2][4], tot[5];
+        uint64_t n[8][3], tot[5];
+        run_bin<1>(t[0], n[0]);
+        run_bin<N>(t[1], n[1]);
+        run_bin<N + 1>(t[2], n[2]);
+        run_bin<N - 1>(t[3], n[3]);
+        run_bin<-1>(t[4], n[4]);
+        run_bin<-N>(t[5], n[5]);
+        run_bin<-N - 1>(t[6], n[6]);
+        run_bin<-N + 1>(t[7], n[7]);
+        uint64_t s3[4][3];
 #pragma unroll
         for (int i = 0; i < 4; ++i) add_planes<3, 3, 3>(n[i], n[i + 4], s3[i]);  // d and its opposite d + 4
-        add_planes<3, 3, 4>(s3[0], s3[1], s4[0]);
-        add_planes<3, 3, 4>(s3[2], s3[3], s4[1]);
-        add_planes<4, 4, 5>(s4[0], s4[1], tot);
+        sum4_planes(s3, tot);
         uint64_t cand = legal;
 #pragma unroll
         for (int i = 4; i >= 0; --i) {

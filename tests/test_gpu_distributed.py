@@ -111,3 +111,37 @@ def test_two_ranks_on_one_gpu_equal_one_process():
         assert d["total"] == ref.counts().cpu().tolist()
     assert [o["n"] for o in sorted(outs, key=lambda d: d["rank"])] == [4501, 4500]
     assert [sum(x) for x in zip(*(o["local"] for o in outs))] == ref.counts().cpu().tolist()
+
+
+def _bench(args, extra=None):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(extra or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, cwd=ROOT,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 prints exactly one JSON line
+    return json.loads(lines[0])
+
+
+def test_bench_two_ranks_on_one_gpu_equal_one_rank():
+    """bench.py's multi-rank path end to end (the driver's 8-GPU run, rehearsed
+    with 2 ranks sharing cuda:0 over gloo): the launcher, the shards, the timed
+    region, the max-over-ranks reduction and the W/D/L all-gather give a line
+    whose W/D/L equals a one-rank run at the same 262,144 global boards
+    (ppo_run_self_play.py:432-441's tally), with the scaling reading aids
+    filled in.  No scaling number is claimed from it (one GPU, shared)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    common = ["--global-envs", "262144", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-side"]
+    one = _bench(["--gpus", "1"] + common)
+    two = _bench(["--gpus", "2"] + common, {"OTH_BENCH_BACKEND": "gloo", "OTH_BENCH_DEVICE": "0"})
+    assert one["config"]["global_boards"] == two["config"]["global_boards"] == 262144
+    assert two["ranks"] == 2 and two["shared_device"] is True and two["n_gpus"] == 1
+    assert two["config"]["boards_per_gpu"] == 131072 and one["config"]["boards_per_gpu"] == 262144
+    assert two["per_gpu_value"] > 0 and abs(two["per_gpu_value"] * 2 - two["value"]) < 1e-6 * two["value"]
+    solo = two["single_gpu_same_shard"]
+    assert solo["boards"] == 131072 and solo["value"] > 0 and solo["unit"] == "env-steps/s"
+    assert two["wdl"] == one["wdl"] and sum(one["wdl"].values()) > 262144
+    assert two["steps"] == one["steps"] == 3 and two["value"] > 0 and one["value"] > 0
