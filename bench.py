@@ -605,26 +605,37 @@ def step_observe_lines(E, n, dev, stream, plies=32):
     don = torch.empty(E, dtype=torch.uint8, device=dev)
     ob = torch.empty(E, n, n, dtype=torch.int64, device=dev)
     ms = torch.empty(E, 4, n, n, dtype=torch.float32, device=dev)
+    ms8 = torch.empty(E, 4, n, n, dtype=torch.int8, device=dev)
+    ms16 = torch.empty(E, 4, n, n, dtype=torch.bfloat16, device=dev)
     a = torch.empty(E, dtype=torch.int32, device=dev)
     lp = torch.empty(E, dtype=torch.float32, device=dev)
     en = torch.empty(E, dtype=torch.float32, device=dev)
     logits = torch.randn(E, NN, device=dev, generator=torch.Generator(device=dev).manual_seed(0))
 
-    def ss(i, obs=False):
+    def ss(i, obs=None):
         return env.sample_step(logits, actions=a, log_probs=lp, entropy=en, rewards=rew, dones=don,
-                               **({"observe": "make_state", "obs": ms} if obs else {}))
+                               **({"observe": "make_state", "obs": obs} if obs is not None else {}))
     t = {"step_board_fused": lambda i: env.step(acts[i], rewards=rew, dones=don, obs=ob),
          "step_board_split": lambda i: (env.step(acts[i], rewards=rew, dones=don, observe=False),
                                         env.observe("board", torch.int64, out=ob)),
          "step_only": lambda i: env.step(acts[i], rewards=rew, dones=don, observe=False),
-         "sample_step_make_state_fused": lambda i: ss(i, True),
+         "sample_step_make_state_fused": lambda i: ss(i, ms),
          "sample_step_make_state_split": lambda i: (ss(i), env.observe("make_state", torch.float32, out=ms)),
-         "sample_step_only": lambda i: ss(i)}
+         "sample_step_only": lambda i: ss(i),
+         # make_state in int8 / bfloat16 (exact for its 0 / 1 planes): a quarter / half the bytes
+         "sample_step_make_state_i8_fused": lambda i: ss(i, ms8),
+         "sample_step_make_state_bf16_fused": lambda i: ss(i, ms16),
+         # what an f32 / bf16 consumer pays to widen the int8 planes into its first layer's input
+         "cast_i8_to_f32": lambda i: ms.copy_(ms8),
+         "cast_i8_to_bf16": lambda i: ms16.copy_(ms8)}
     us = {k: _graph_us(env, start, fn, plies, stream) for k, fn in t.items()}
     env.close()
     step_b = 40 * W + 11
     b_board = E * (step_b + 8 * NN)
-    b_ms = E * (4 * NN + 12 + step_b + 4 * 4 * NN)
+
+    def b_ply(esize):  # the learners' ply: logits in, the sample out, the step, make_state written
+        return E * (4 * NN + 12 + step_b + 4 * esize * NN)
+    b_ms = b_ply(4)
 
     def frac(b, u):
         return _r(b / (u * 1e-6) / 1e9 / HBM_PEAK_GBPS)
@@ -642,6 +653,17 @@ def step_observe_lines(E, n, dev, stream, plies=32):
                                        "algorithmic_bytes_per_board": 4 * NN + 12 + step_b + 16 * NN,
                                        "frac": frac(b_ms, us["sample_step_make_state_fused"]),
                                        "pmc": pmc_ref("sample-step-make-state-f32-%dx%d-E%d" % (n, n, E))},
+            "sample_step_make_state_narrow": {
+                "kernel": "k_sample_step2<%d> + obs tail" % n,
+                "i8_us_per_ply": _r(us["sample_step_make_state_i8_fused"]),
+                "i8_bytes_per_board": 4 * NN + 12 + step_b + 4 * NN,
+                "i8_frac": frac(b_ply(1), us["sample_step_make_state_i8_fused"]),
+                "bf16_us_per_ply": _r(us["sample_step_make_state_bf16_fused"]),
+                "bf16_bytes_per_board": 4 * NN + 12 + step_b + 8 * NN,
+                "bf16_frac": frac(b_ply(2), us["sample_step_make_state_bf16_fused"]),
+                "cast_i8_to_f32_us": _r(us["cast_i8_to_f32"]), "cast_i8_to_bf16_us": _r(us["cast_i8_to_bf16"]),
+                "note": "make_state is 0 / 1: exact in int8 and bfloat16; the cast lines are torch's copy_ of the "
+                        "int8 planes into an f32 / bf16 tensor of the same shape (a consumer widening them)"},
             "timing": "HIP graph of %d calls from one mid-game state, median of 5 replays" % plies}
 
 
@@ -691,6 +713,10 @@ def side_summary(side, out):
             summ[k] = {"us_per_ply": so[k]["us_per_ply"], "two_launch_us": so[k]["two_launch_us"],
                        "frac": so[k]["frac"]}
         summ["sample_step"] = {"us_per_ply": so["us"]["sample_step_only"]}
+        nw = so.get("sample_step_make_state_narrow")
+        if nw:
+            summ["sample_step_make_state_i8"] = {"us_per_ply": nw["i8_us_per_ply"], "frac": nw["i8_frac"]}
+            summ["sample_step_make_state_bf16"] = {"us_per_ply": nw["bf16_us_per_ply"], "frac": nw["bf16_frac"]}
     for x in side.get("othello_env_vs", []):
         summ["othello_env_vs_" + x["opponent"]] = {"us_per_call": _r(x["us_per_call"]),
                                                    "env_steps_per_s": _r(x["env_steps_per_s"])}
@@ -841,8 +867,8 @@ def observe_bytes(n, E, layout, esize):
     the board words (16W), meta (2) and, for the layouts with a legal plane,
     possible_moves (8W) read once per board."""
     W = (n * n + 63) // 64
-    planes = {"board": 1, "board_legal": 2, "make_state": 4, "absolute": 1}[layout]
-    reads = 16 * W + 2 + (8 * W if layout in ("board_legal", "make_state") else 0)
+    planes = {"board": 1, "board_legal": 2, "make_state": 4, "absolute": 1, "legal": 1}[layout]
+    reads = 16 * W + 2 + (8 * W if layout in ("board_legal", "make_state", "legal") else 0)
     return E * (planes * n * n * esize + reads)
 
 

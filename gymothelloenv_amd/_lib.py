@@ -32,7 +32,7 @@ OTH_OBS_BOARD_LEGAL = 1
 OTH_OBS_MAKE_STATE = 2
 OTH_OBS_ABSOLUTE = 3
 OTH_OBS_LEGAL = 4
-OTH_I8, OTH_I32, OTH_I64, OTH_F32, OTH_F64 = range(5)
+OTH_I8, OTH_I32, OTH_I64, OTH_F32, OTH_F64, OTH_BF16 = range(6)
 OTH_MASKED_SAMPLE, OTH_MASKED_MODE, OTH_MASKED_EVAL = range(3)
 OTH_MASKED_FULL_ENTROPY = 4
 OTH_GRAPH_SLOTS = 64

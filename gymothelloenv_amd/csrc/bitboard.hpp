@@ -601,6 +601,59 @@ OTH_HD DW<K> sh(const DW<K>& x) {
     return y;
 }
 
+// a + b and y - 1 on K dwords, the carry / borrow passed along (v_add_co_u32 /
+// v_sub_co_u32, then v_addc_co_u32 / v_subb_co_u32 per dword)
+template <int K>
+OTH_HD DW<K> add_dw(const DW<K>& a, const DW<K>& b) {
+    DW<K> r;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+#if defined(__clang__)
+        r.d[i] = __builtin_addc(a.d[i], b.d[i], c, &c);
+#else
+        const uint64_t x = (uint64_t)a.d[i] + b.d[i] + c;
+        r.d[i] = (uint32_t)x;
+        c = (uint32_t)(x >> 32);
+#endif
+    }
+    return r;
+}
+template <int K>
+OTH_HD DW<K> dec_dw(const DW<K>& y) {
+    DW<K> r;
+    uint32_t b = 0;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+#if defined(__clang__)
+        r.d[i] = __builtin_subc(y.d[i], i == 0 ? 1u : 0u, b, &b);
+#else
+        const uint64_t x = (uint64_t)y.d[i] - (i == 0 ? 1u : 0u) - b;
+        r.d[i] = (uint32_t)x;
+        b = (uint32_t)(x >> 63);
+#endif
+    }
+    return r;
+}
+OTH_HD uint32_t rev32(uint32_t x) {
+#if defined(__clang__)
+    return __builtin_bitreverse32(x);
+#else
+    return (uint32_t)(rev64(x) >> 32);
+#endif
+}
+// Square a -> NN - 1 - a (the board turned by 180 degrees: rows stay rows,
+// reversed; an involution) on K dwords: the dwords bit-reversed in reverse
+// order (v_bfrev_b32), then moved down past the 32K - NN unused bits.
+template <int N, int K>
+OTH_HD DW<K> turn_dw(const DW<K>& x) {
+    static_assert(32 * K >= N * N && 32 * K - N * N < 64, "the board's words");
+    DW<K> r;
+#pragma unroll
+    for (int j = 0; j < K; ++j) r.d[j] = rev32(x.d[K - 1 - j]);
+    return sh<-(32 * K - N * N)>(r);
+}
+
 // legal_axis on dwords (the same steps, propagators and reuse)
 template <int N, int S, int K = 2 * Geo<N>::W>
 OTH_HD void legal_axis_dw(const DW<K>& P, const DW<K>& p1, DW<K>& L, DW<K>& tplus, DW<K>& tminus) {
@@ -651,6 +704,23 @@ OTH_HD void legal_axis_dw(const DW<K>& P, const DW<K>& p1, DW<K>& L, DW<K>& tplu
     }
 }
 
+// The horizontal axis of legal_axis_dw by carries (OneWord::axis_h on K dwords):
+// stepping +1 from an own disc through a run of inner-column opponent discs is
+// the carry chain of (P << 1) + pin, which clears the run and sets the square
+// past it, so that fill is pin & ~((P << 1) + pin) -- a shift, a K-dword add
+// and an and-not per dword instead of the Kogge-Stone chain and its
+// propagators; stepping -1 is the same on the board turned by 180 degrees
+// (turn_dw).  No carry crosses a row: pin holds no edge-column square.
+template <int N, int K>
+OTH_HD void axis_h_dw(const DW<K>& P, const DW<K>& pin, DW<K>& L, DW<K>& tplus, DW<K>& tminus) {
+    const DW<K> fe = pin & ~add_dw(sh<1>(P), pin);
+    const DW<K> rpin = turn_dw<N>(pin);
+    const DW<K> fw = turn_dw<N>(rpin & ~add_dw(sh<1>(turn_dw<N>(P)), rpin));
+    tplus = fe;
+    tminus = fw;
+    L = L | sh<1>(fe) | sh<-1>(fw);
+}
+
 // legal_moves_fills for multi-word boards on dwords (fills returned as words)
 template <int N>
 OTH_HD BB<Geo<N>::W> legal_moves_fills_dw(const BB<Geo<N>::W>& Pb, const BB<Geo<N>::W>& Ob, BB<Geo<N>::W> t[8]) {
@@ -658,7 +728,7 @@ OTH_HD BB<Geo<N>::W> legal_moves_fills_dw(const BB<Geo<N>::W>& Pb, const BB<Geo<
     static_assert(W >= 2, "multi-word boards");
     const DW<K> P = to_dw<W>(Pb), O = to_dw<W>(Ob), pin = O & to_dw<W>(Geo<N>::INNER);
     DW<K> L{}, f[8];
-    legal_axis_dw<N, 1>(P, pin, L, f[4], f[0]);
+    axis_h_dw<N>(P, pin, L, f[4], f[0]);  // 10x10 random play: 1.632 -> 1.536 us per ply (profiles/r06/d)
     legal_axis_dw<N, N>(P, O, L, f[5], f[1]);
     legal_axis_dw<N, N + 1>(P, pin, L, f[6], f[2]);
     legal_axis_dw<N, N - 1>(P, pin, L, f[7], f[3]);
@@ -668,44 +738,35 @@ OTH_HD BB<Geo<N>::W> legal_moves_fills_dw(const BB<Geo<N>::W>& Pb, const BB<Geo<
 }
 
 // update_board's flips (othello.py:391-410) from the fills of the side to
-// move and the ray table rays[d * N*N + a] (the squares strictly beyond a in
-// direction d): along ray d the run to flip is the part of the ray before its
-// first square outside t[d] (every fill square on that run is capped further
-// along d).  Toward higher squares that square is the lowest set bit of
-// ray & ~t[d] over the words in ascending order, toward lower squares the
-// highest over the words in descending order.  The last square of a ray is
-// never in a fill, so a non-empty ray always has one.
+// move (t[d]: the opponent discs from which an own disc is reached going along
+// d) and the ray table rays[d * N*N + a] (the squares strictly beyond a in
+// direction d), on dwords: along each ray direction d toward higher squares the
+// run is ray & t[d] & (y - 1) with y = ray & ~t[d] (y - 1 a K-dword decrement:
+// its lowest set bit, the first ray square outside the fill, cleared and every
+// bit below it set); toward lower squares the same on the board turned by 180
+// degrees, where the ray of d from a is the ray of the opposite direction d - 4
+// from NN - 1 - a (the table's "up" half) and the fill is turn_dw(t[d]); the
+// four turned runs are turned back once.  No count-leading-zeros, no per-word
+// found / carry selects (round 5's word-by-word form with a lowest / highest set
+// bit per word: 10x10 random play 1.588 -> 1.536 us per ply, profiles/r06/d).
 template <int N>
 OTH_HD BB<Geo<N>::W> flips_fills(const BB<Geo<N>::W>* rays, const BB<Geo<N>::W> t[8], int a) {
-    constexpr int W = Geo<N>::W;
-    constexpr int NN = N * N;
-    auto f = zero<W>();
+    constexpr int W = Geo<N>::W, K = 2 * W, NN = N * N;
+    DW<K> up{}, dn{};
+    const int ta = NN - 1 - a;
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
-        const BB<W> ray = rays[d * NN + a];
-        bool found = false;
-#pragma unroll
-        for (int i = 0; i < W; ++i) {
-            const uint64_t y = ray.w[i] & ~t[d].w[i];
-            const uint64_t fi = ray.w[i] & ((y & (0ull - y)) - 1ull);  // y == 0: the whole word
-            f.w[i] |= found ? 0ull : fi;
-            found = found || y != 0ull;
-        }
+        const DW<K> ray = to_dw<W>(rays[d * NN + a]), td = to_dw<W>(t[d]);
+        const DW<K> run = ray & td & dec_dw(ray & ~td);
+        up = up | run;
     }
 #pragma unroll
     for (int d = 4; d < 8; ++d) {
-        const BB<W> ray = rays[d * NN + a];
-        bool found = false;
-#pragma unroll
-        for (int i = W - 1; i >= 0; --i) {
-            const uint64_t y = ray.w[i] & ~t[d].w[i];
-            const uint64_t hb = 0x8000000000000000ull >> clz64(y | 1ull);
-            const uint64_t fi = y ? (ray.w[i] & (0ull - (hb << 1))) : ray.w[i];
-            f.w[i] |= found ? 0ull : fi;
-            found = found || y != 0ull;
-        }
+        const DW<K> ray = to_dw<W>(rays[(d - 4) * NN + ta]), td = turn_dw<N>(to_dw<W>(t[d]));
+        const DW<K> run = ray & td & dec_dw(ray & ~td);
+        dn = dn | run;
     }
-    return f;
+    return to_bb<K>(up | turn_dw<N>(dn));
 }
 
 // GreedyPolicy on bit planes for any W (OneWord::greedy's algorithm on BB<W>):
@@ -1108,21 +1169,25 @@ OTH_HD int select64_tab(uint64_t x, int k, const uint8_t* sel8) {
 #endif
     return (up ? 32 : 0) + 8 * b + sel8[8 * byte + (uint32_t)(kk - qb)];
 }
-// select_bit with select64_tab inside the word (k < popcount: a pick from a non-empty mask)
+// select_bit with select64_tab inside the word (k < popcount: a pick from a
+// non-empty mask), without branches: the word holding the k-th set bit picked by
+// selects on the words' prefix counts, then ONE select64_tab.  A word-by-word
+// loop compiles to an exec-masked region per word, each run whenever some lane
+// of the wave picks in that word (two-word random play ran both on almost every
+// ply): 10x10 random play 1.540 -> 1.437 us per ply (profiles/r06/e).
 template <int W>
 OTH_HD int select_bit_tab(const BB<W>& b, int k, const uint8_t* sel8) {
-    int res = 0;
-    bool found = false;
+    uint64_t x = b.w[0];
+    int kk = k, base = 0, pre = 0;
 #pragma unroll
-    for (int i = 0; i < W; ++i) {
-        const int c = popc64(b.w[i]);
-        if (!found && k < c) {
-            res = 64 * i + select64_tab(b.w[i], k, sel8);
-            found = true;
-        }
-        if (!found) k -= c;
+    for (int i = 1; i < W; ++i) {
+        pre += popc64(b.w[i - 1]);
+        const bool up = k >= pre;
+        x = up ? b.w[i] : x;
+        kk = up ? k - pre : kk;
+        base = up ? 64 * i : base;
     }
-    return res;
+    return base + select64_tab(x, kk, sel8);
 }
 template <int W>
 OTH_HD int select_bit(const BB<W>& b, int k) {

@@ -314,7 +314,7 @@ int oth_step_observe(oth_env* env, const int32_t* actions, int32_t* rewards, uin
     OTH_CHECK_ENV(env);
     if (!actions || !obs) return fail(OTH_EINVAL, "actions / obs is NULL");
     if (layout < OTH_OBS_BOARD || layout > OTH_OBS_LEGAL) return fail(OTH_EINVAL, "unknown layout");
-    if (dtype < OTH_I8 || dtype > OTH_F64) return fail(OTH_EINVAL, "unknown dtype");
+    if (dtype < OTH_I8 || dtype > OTH_BF16) return fail(OTH_EINVAL, "unknown dtype");
     const uint64_t ply = env->ply++;
     return with_n(env->n, [&](auto NC) {
         return launch_step_observe<decltype(NC)::value>(env, actions, rewards, dones, layout, dtype, obs, ply,
@@ -423,7 +423,7 @@ int oth_step_vs_observe(oth_env* env, int32_t opponent_policy, const int32_t* ac
     if (opponent_policy < OTH_POLICY_RANDOM || opponent_policy > OTH_POLICY_LAST)
         return fail(OTH_EINVAL, "unknown opponent policy");
     if (layout < OTH_OBS_BOARD || layout > OTH_OBS_LEGAL) return fail(OTH_EINVAL, "unknown layout");
-    if (dtype < OTH_I8 || dtype > OTH_F64) return fail(OTH_EINVAL, "unknown dtype");
+    if (dtype < OTH_I8 || dtype > OTH_BF16) return fail(OTH_EINVAL, "unknown dtype");
     if (int rc = maximin_budget(env, opponent_policy, 2.0, MM_STEP_VS, (hipStream_t)stream)) return rc;
     const uint64_t call = env->ply++;
     return with_n(env->n, [&](auto NC) {
@@ -516,7 +516,7 @@ int oth_sample_step_observe(oth_env* env, const float* logits, int64_t ld, const
     if (base != OTH_MASKED_SAMPLE && base != OTH_MASKED_MODE) return fail(OTH_EINVAL, "mode must be SAMPLE or MODE");
     if (ld < (int64_t)env->n * env->n) return fail(OTH_EINVAL, "ld < N*N");
     if (layout < OTH_OBS_BOARD || layout > OTH_OBS_LEGAL) return fail(OTH_EINVAL, "unknown layout");
-    if (dtype < OTH_I8 || dtype > OTH_F64) return fail(OTH_EINVAL, "unknown dtype");
+    if (dtype < OTH_I8 || dtype > OTH_BF16) return fail(OTH_EINVAL, "unknown dtype");
     const uint64_t ply = env->ply++;
     return with_n(env->n, [&](auto NC) {
         return launch_sample_step<decltype(NC)::value>(env, logits, (long long)ld, uniforms, counter, mode, actions,
@@ -589,7 +589,7 @@ int oth_observe(oth_env* env, int32_t layout, int32_t dtype, void* out, oth_stre
     OTH_CHECK_ENV(env);
     if (!out) return fail(OTH_EINVAL, "out is NULL");
     if (layout < OTH_OBS_BOARD || layout > OTH_OBS_LEGAL) return fail(OTH_EINVAL, "unknown layout");
-    if (dtype < OTH_I8 || dtype > OTH_F64) return fail(OTH_EINVAL, "unknown dtype");
+    if (dtype < OTH_I8 || dtype > OTH_BF16) return fail(OTH_EINVAL, "unknown dtype");
     return with_n(env->n, [&](auto NC) {
         return launch_observe<decltype(NC)::value>(env, layout, dtype, out, (hipStream_t)stream);
     });

@@ -1705,6 +1705,15 @@ __global__ __launch_bounds__(BLOCK) void k_count(const uint64_t* __restrict__ bo
     out[2 * (size_t)e + 1] = b;
 }
 
+// A bfloat16 observation element (OTH_BF16).  The observations hold -1, 0 and
+// +1 only, each exact in bfloat16: 0xBF80, 0x0000, 0x3F80.
+struct obs_bf16 {
+    uint16_t bits;
+    obs_bf16() = default;
+    __host__ __device__ explicit obs_bf16(int v) : bits(v == 0 ? 0u : (v > 0 ? 0x3F80u : 0xBF80u)) {}
+};
+static_assert(sizeof(obs_bf16) == 2, "a bfloat16");
+
 template <typename T>
 __device__ __forceinline__ void put(void* out, size_t i, int v) {
     reinterpret_cast<T*>(out)[i] = (T)v;
@@ -1760,13 +1769,14 @@ __global__ __launch_bounds__(BLOCK) void k_observe(const uint64_t* __restrict__ 
             case OTH_I32: put<int32_t>(out, i, v); break;
             case OTH_I64: put<int64_t>(out, i, v); break;
             case OTH_F32: put<float>(out, i, v); break;
+            case OTH_BF16: put<obs_bf16>(out, i, v); break;
             default: put<double>(out, i, v); break;
         }
     }
 }
 
 // A quad of 4 consecutive squares of one plane as one vector store (16 B for
-// f32 / i32, 4 B for i8, 2 x 16 B for the 8-byte types): k_observe_w's unit
+// f32 / i32, 8 B for bf16, 4 B for i8, 2 x 16 B for the 8-byte types): k_observe_w's unit
 // (the 8-byte types take pairs of squares instead, OTH_OBS_PAIR8).
 // (as streaming stores: 65,536 boards 2-3 % slower, 1,048,576 int64 boards 104 -> 250 us;
 // profiles/r04/d/ab_obs_nt.jsonl)
@@ -1776,6 +1786,11 @@ __device__ __forceinline__ void put_quad(T* out, uint32_t q, int v0, int v1, int
         const uint32_t x = (uint32_t)(uint8_t)(int8_t)v0 | ((uint32_t)(uint8_t)(int8_t)v1 << 8) |
                            ((uint32_t)(uint8_t)(int8_t)v2 << 16) | ((uint32_t)(uint8_t)(int8_t)v3 << 24);
         reinterpret_cast<uint32_t*>(out)[q] = x;
+    } else if constexpr (sizeof(T) == 2) {
+        uint2 x;
+        x.x = (uint32_t)T(v0).bits | ((uint32_t)T(v1).bits << 16);
+        x.y = (uint32_t)T(v2).bits | ((uint32_t)T(v3).bits << 16);
+        reinterpret_cast<uint2*>(out)[q] = x;
     } else if constexpr (sizeof(T) == 4) {
         using V4 = typename std::conditional<std::is_same<T, float>::value, float4, int4>::type;
         V4 x;
@@ -1796,6 +1811,35 @@ __device__ __forceinline__ void put_quad(T* out, uint32_t q, int v0, int v1, int
     }
 }
 
+// S one- or two-byte observation elements of one unit (+1 where pos, -1 where
+// neg, 0 elsewhere: bit j of the masks is square j of the unit) as ONE store of
+// S * sizeof(T) bytes.  Each dword spreads 4 bits into bytes (bit i of x < 16
+// lands in byte i of x * 0x204081 & 0x01010101) or 2 bits into halves (x * 0x8001
+// & 0x10001), then scales: 0xFF (int8 -1), 0x3F80 / 0xBF80 (bf16 +1 / -1).
+template <typename T, int S>
+__device__ __forceinline__ void put_narrow(T* out, uint32_t g, uint32_t pos, uint32_t neg) {
+    static_assert(sizeof(T) <= 2 && (S * sizeof(T)) % 4 == 0 && S * sizeof(T) <= 16, "one store of 4 to 16 bytes");
+    constexpr int D = (int)(S * sizeof(T) / 4);
+    uint32_t d[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        if constexpr (sizeof(T) == 1) {
+            const uint32_t p = (pos >> (4 * k)) & 0xFu, n = (neg >> (4 * k)) & 0xFu;
+            d[k] = ((p * 0x204081u) & 0x01010101u) | (((n * 0x204081u) & 0x01010101u) * 0xFFu);
+        } else {
+            const uint32_t p = (pos >> (2 * k)) & 3u, n = (neg >> (2 * k)) & 3u;
+            d[k] = ((p * 0x8001u) & 0x10001u) * 0x3F80u | ((n * 0x8001u) & 0x10001u) * 0xBF80u;
+        }
+    }
+    if constexpr (D == 4) {
+        reinterpret_cast<uint4*>(out)[g] = make_uint4(d[0], d[1], d[2], d[3]);
+    } else if constexpr (D == 2) {
+        reinterpret_cast<uint2*>(out)[g] = make_uint2(d[0], d[1]);
+    } else {
+        reinterpret_cast<uint32_t*>(out)[g] = d[0];
+    }
+}
+
 #ifndef OTH_OBS_PAIR8
 // 8-byte observations by pairs of squares, one 16-B store per lane (1 KiB
 // contiguous per store instruction) instead of quads in two 16-B stores (each
@@ -1804,6 +1848,14 @@ __device__ __forceinline__ void put_quad(T* out, uint32_t q, int v0, int v1, int
 // tensor: 8.95; profiles/r05/i/ab_step_obs.json)
 #define OTH_OBS_PAIR8 1
 #endif
+// obs_stream's squares per lane and store for NN squares of esize-byte elements
+// (below), and the byte alignment the output needs for them
+__host__ __device__ constexpr int obs_unit(int NN, int esize) {
+    return esize == 8 ? (OTH_OBS_PAIR8 ? 2 : 4) : (NN % (16 / esize) == 0 ? 16 / esize : 4);
+}
+__host__ __device__ constexpr int obs_align(int NN, int esize) {
+    return obs_unit(NN, esize) * esize > 4 * esize ? obs_unit(NN, esize) * esize : 4 * esize;
+}
 template <int LAYOUT>
 constexpr int obs_planes() {
     return LAYOUT == OTH_OBS_BOARD_LEGAL ? 2 : (LAYOUT == OTH_OBS_MAKE_STATE ? 4 : 1);
@@ -1864,10 +1916,17 @@ __device__ __forceinline__ void obs_stream(const uint64_t (&bw)[Geo<N>::W], cons
     // unrolled by 4 +-0 (by 2 / 4 on the branch-free body: +-0, profiles/r04/obs/ab_unroll_bf.jsonl); 128 / 256 boards per wave (every wave resident at once, all
     // loads first) 218.8 -> 216.6 / 234.4, and at 262,144 boards 46.5 -> 57.6 / 110.3
     // (profiles/r04/obs/)
-    // S squares per lane and store: quads (S = 4), or for the 8-byte types under
-    // OTH_OBS_PAIR8 pairs (S = 2: one 16-B store per lane, so each store
-    // instruction writes 1 KiB contiguous instead of two half-filled 2-KiB spans)
-    constexpr int S = (sizeof(T) == 8 && OTH_OBS_PAIR8) ? 2 : 4;
+    // S squares per lane and store: 16 bytes a lane where a plane divides into such
+    // units -- 16 squares of int8, 8 of bf16, quads of the 4-byte types, and for the
+    // 8-byte types under OTH_OBS_PAIR8 pairs (one 16-B store per lane, so each store
+    // instruction writes 1 KiB contiguous instead of two half-filled 2-KiB spans) --
+    // else quads.  One- and two-byte units are packed from their bit masks
+    // (put_narrow): at 65,536 8x8 boards the learners' fused ply with its make_state
+    // 15.43 -> 10.03 us per graphed ply in int8 (quads: a 4-B store per lane; the
+    // sample-step alone 6.2), 17.25 -> 13.34 in bf16; k_observe_w make_state int8
+    // 9.54 -> 5.36 us, 1,048,576 boards 86.6 -> 50.0 (profiles/r06/e)
+    constexpr int S = obs_unit(NN, (int)sizeof(T));
+    constexpr bool NARROW = sizeof(T) <= 2;
     constexpr uint32_t UQ = (uint32_t)(NN / S), UB = (uint32_t)obs_planes<LAYOUT>() * UQ;  // units per plane / board
     constexpr uint32_t SM = (1u << S) - 1u;
     const int totalu = nb * (int)UB;
@@ -1891,6 +1950,26 @@ __device__ __forceinline__ void obs_stream(const uint64_t (&bw)[Geo<N>::W], cons
         // between them): make_state f32 at 65,536 / 262,144 / 1,048,576 boards
         // 13.75 -> 12.79 / 46.6 -> 41.5 / 219.8 -> 208.3 us, int64 board 1,048,576
         // 104.7 -> 102.4 (profiles/r04/obs/ab_branchfree.jsonl)
+        if constexpr (NARROW) {  // +1 where pos, -1 where neg, packed a dword at a time
+            uint32_t pos, neg = 0u;
+            if constexpr (LAYOUT == OTH_OBS_LEGAL) {
+                pos = (uint32_t)(xl >> bi) & SM;
+            } else if constexpr (LAYOUT == OTH_OBS_ABSOLUTE) {
+                pos = (uint32_t)(xw >> bi) & SM;
+                neg = (uint32_t)(xb >> bi) & SM;
+            } else if constexpr (LAYOUT == OTH_OBS_MAKE_STATE) {
+                const uint64_t m0 = 0ull - (uint64_t)(plane == 0u), m1 = 0ull - (uint64_t)(plane == 1u);
+                const uint64_t m2 = 0ull - (uint64_t)(plane == 2u && tw), m3 = 0ull - (uint64_t)(plane == 3u && (flk & 2u));
+                pos = (uint32_t)(((xb & m0) | (xw & m1) | (xl & m3) | m2) >> bi) & SM;
+            } else {
+                const uint64_t xm = tw ? xw : xb, xo = tw ? xb : xw;
+                const bool p1 = plane != 0u;
+                pos = (uint32_t)((p1 ? xl : xm) >> bi) & SM;
+                neg = p1 ? 0u : (uint32_t)(xo >> bi) & SM;
+            }
+            if (g0 + lane < totalu) put_narrow<T, S>(base, g, pos, neg);
+            continue;
+        }
         int v[4] = {0, 0, 0, 0};
         if constexpr (LAYOUT == OTH_OBS_LEGAL) {  // possible_moves
             const uint32_t nl = (uint32_t)(xl >> bi) & SM;
@@ -1997,6 +2076,9 @@ __device__ __forceinline__ void obs_tail(int layout, int dtype, void* __restrict
                     break;
                 case OTH_F32:
                     obs_stream<N, LAY, float, BPW, LS>(bw, ww, lw, fl, nb, (float*)out + e0 * PER);
+                    break;
+                case OTH_BF16:
+                    obs_stream<N, LAY, obs_bf16, BPW, LS>(bw, ww, lw, fl, nb, (obs_bf16*)out + e0 * PER);
                     break;
                 default:
                     obs_stream<N, LAY, double, BPW, LS>(bw, ww, lw, fl, nb, (double*)out + e0 * PER);

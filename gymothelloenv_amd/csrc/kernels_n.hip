@@ -52,8 +52,9 @@ struct ObsOut {
 // obs_tail's quad stores need N*N % 4 == 0 and an output aligned to 4 elements
 template <int N>
 bool obs_fusable(int dtype, const void* out) {
-    static const int esize[5] = {1, 4, 8, 4, 8};
-    return (N * N) % 4 == 0 && dtype >= OTH_I8 && dtype <= OTH_F64 && (uintptr_t)out % (4 * esize[dtype]) == 0;
+    static const int esize[6] = {1, 4, 8, 4, 8, 2};
+    return (N * N) % 4 == 0 && dtype >= OTH_I8 && dtype <= OTH_BF16 &&
+           (uintptr_t)out % obs_align(N * N, esize[dtype]) == 0;
 }
 
 }  // namespace
@@ -411,16 +412,17 @@ template <int N>
 int launch_observe(oth_env* env, int layout, int dtype, void* out, hipStream_t st) {
     const int planes = layout == OTH_OBS_BOARD_LEGAL ? 2 : (layout == OTH_OBS_MAKE_STATE ? 4 : 1);
     const long long total = (long long)env->E * planes * N * N;
-    static const int esize[5] = {1, 4, 8, 4, 8};
+    static const int esize[6] = {1, 4, 8, 4, 8, 2};
     if constexpr ((N * N) % 4 == 0) {
         // vector stores need a 4-element-aligned base and 32-bit quad indices
-        if (dtype >= OTH_I8 && dtype <= OTH_F64 && (uintptr_t)out % (4 * esize[dtype]) == 0 &&
+        if (dtype >= OTH_I8 && dtype <= OTH_BF16 && (uintptr_t)out % obs_align(N * N, esize[dtype]) == 0 &&
             total / 4 < (1ll << 31)) {
             switch (dtype) {
                 case OTH_I8: launch_observe_w<N, int8_t>(env, layout, out, st); break;
                 case OTH_I32: launch_observe_w<N, int32_t>(env, layout, out, st); break;
                 case OTH_I64: launch_observe_w<N, long long>(env, layout, out, st); break;
                 case OTH_F32: launch_observe_w<N, float>(env, layout, out, st); break;
+                case OTH_BF16: launch_observe_w<N, obs_bf16>(env, layout, out, st); break;
                 default: launch_observe_w<N, double>(env, layout, out, st); break;
             }
             return after_launch("oth_observe");

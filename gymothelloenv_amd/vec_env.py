@@ -21,7 +21,7 @@ _OBS_PLANES = {L.OTH_OBS_BOARD: 1, L.OTH_OBS_BOARD_LEGAL: 2, L.OTH_OBS_MAKE_STAT
                L.OTH_OBS_LEGAL: 1}
 _ONE_PLANE = (L.OTH_OBS_BOARD, L.OTH_OBS_ABSOLUTE, L.OTH_OBS_LEGAL)
 _DTYPES = {torch.int8: L.OTH_I8, torch.int32: L.OTH_I32, torch.int64: L.OTH_I64,
-           torch.float32: L.OTH_F32, torch.float64: L.OTH_F64}
+           torch.float32: L.OTH_F32, torch.float64: L.OTH_F64, torch.bfloat16: L.OTH_BF16}
 _POLICIES = {"random": L.OTH_POLICY_RANDOM, "greedy": L.OTH_POLICY_GREEDY}
 _POLICIES.update({"maximin%d" % d: L.OTH_POLICY_MAXIMIN(d) for d in range(1, L.OTH_MAXIMIN_MAX_DEPTH + 1)})
 

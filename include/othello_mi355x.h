@@ -90,8 +90,10 @@ enum {
     OTH_OBS_LEGAL = 4        /* (E,N,N)   possible_moves as 0 / 1 (othello.py:313-343; the plane of
                                           OTH_OBS_BOARD_LEGAL alone: int8 views as a bool mask) */
 };
-/* observation element types */
-enum { OTH_I8 = 0, OTH_I32 = 1, OTH_I64 = 2, OTH_F32 = 3, OTH_F64 = 4 };
+/* observation element types; OTH_BF16 is bfloat16 (the observations' values
+ * -1 / 0 / +1 are exact in it): half the bytes of float32 for a network that
+ * takes bfloat16 input, e.g. make_state for a learner under bf16 autocast */
+enum { OTH_I8 = 0, OTH_I32 = 1, OTH_I64 = 2, OTH_F32 = 3, OTH_F64 = 4, OTH_BF16 = 5 };
 
 /* masked-categorical modes (oth_masked_sample) */
 enum {

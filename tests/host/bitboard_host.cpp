@@ -93,6 +93,7 @@ static void greedy_planes_w_n(int E, const uint64_t* mover, const uint64_t* opp,
     }
 }
 
+
 #define DISPATCH8(fn, ...)                 \
     switch (n) {                           \
         case 4: fn<4>(__VA_ARGS__); break; \
@@ -157,6 +158,21 @@ int host_select_tab(uint64_t x, int k) {
         init = true;
     }
     return select64_tab(x, k, reinterpret_cast<const uint8_t*>(tab));
+}
+// select_bit_tab (the multi-word branch-free random pick) on W = 2..4 words
+int host_select_tab_w(const uint64_t* words, int W, int k) {
+    static uint64_t tab[256];
+    static bool init = false;
+    if (!init) {
+        for (int i = 0; i < 256; ++i) tab[i] = sel8_word((uint32_t)i);
+        init = true;
+    }
+    const uint8_t* t = reinterpret_cast<const uint8_t*>(tab);
+    BB<4> b;
+    for (int i = 0; i < 4; ++i) b.w[i] = i < W ? words[i] : 0;
+    if (W == 2) return select_bit_tab<2>(*reinterpret_cast<const BB<2>*>(b.w), k, t);
+    if (W == 3) return select_bit_tab<3>(*reinterpret_cast<const BB<3>*>(b.w), k, t);
+    return select_bit_tab<4>(b, k, t);
 }
 void host_philox4(uint64_t seed, uint32_t id, uint64_t ctr, uint32_t purpose, uint32_t* out) {
     U4 u = philox4(seed, id, ctr, purpose);

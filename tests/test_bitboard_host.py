@@ -87,6 +87,24 @@ def test_flips_host_build(hostlib, n):
     np.testing.assert_array_equal(out, opp & ~s.boards[:, :W])
 
 
+@pytest.mark.parametrize("W", [2, 3, 4])
+def test_select_multiword_branch_free(hostlib, W):
+    """select_bit_tab (two-word random play's pick: the word by selects on the
+    prefix counts, then one select64_tab) gives every rank k of sparse and dense
+    masks, empty words included."""
+    f = hostlib.host_select_tab_w
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    rng = np.random.RandomState(40 + W)
+    for _ in range(600):
+        dens = rng.choice([0.0, 0.03, 0.15, 0.5, 0.95])
+        words = np.array([int(sum(1 << i for i in range(64) if rng.rand() < dens)) for _ in range(W)], dtype=np.uint64)
+        if rng.rand() < 0.3:
+            words[rng.randint(W)] = 0
+        bits = [64 * w + i for w in range(W) for i in range(64) if (int(words[w]) >> i) & 1]
+        for k, b in enumerate(bits):
+            assert f(ptr(words), W, k) == b, (W, [hex(int(x)) for x in words], k)
+
+
 @pytest.mark.parametrize("variant", ["select64", "select64_tab"])
 def test_select_variants_every_rank(hostlib, variant):
     """Both select forms (byte-parallel select64, and select64_tab with the bit

@@ -619,6 +619,17 @@ def _obs_np(n, boards, meta, legal, layout):
     return np.stack([b, w, np.broadcast_to(tw.astype(np.int64), b.shape), ms_legal], 1).reshape(E, 4, n, n)
 
 
+def _host(o):
+    """An observation as numpy; bfloat16 (absent from numpy) as float32 after
+    checking its bit patterns are exactly bfloat16's -1 / 0 / +1."""
+    import torch
+    if o.dtype == torch.bfloat16:
+        bits = o.view(torch.int16).cpu().numpy()
+        assert np.isin(bits, [0, 0x3F80, 0xBF80 - 0x10000]).all()
+        return o.float().cpu().numpy()
+    return o.cpu().numpy()
+
+
 @pytest.mark.parametrize("n", [4, 5, 7, 8, 10, 16])
 def test_observation_kernels_every_layout_and_alignment(torch_cuda, n):
     """Vector-store quad kernel (N*N % 4 == 0, aligned out) and the scalar kernel
@@ -631,13 +642,13 @@ def test_observation_kernels_every_layout_and_alignment(torch_cuda, n):
     b, m, lg = get_state_np(env)
     for layout in ("board", "board_legal", "make_state", "absolute", "legal"):
         want = _obs_np(n, b, m, lg, layout)
-        for dt in (torch.int8, torch.int32, torch.int64, torch.float32, torch.float64):
+        for dt in (torch.int8, torch.int32, torch.int64, torch.float32, torch.float64, torch.bfloat16):
             got = env.observe(layout, dt)
-            np.testing.assert_array_equal(got.cpu().numpy(), want, err_msg="%s %s" % (layout, dt))
+            np.testing.assert_array_equal(_host(got), want, err_msg="%s %s" % (layout, dt))
             buf = torch.empty(want.size + 1, dtype=dt, device=got.device)
             off = buf[1:].view(want.shape)  # base one element past the vector alignment
             env.observe(layout, dt, out=off)
-            np.testing.assert_array_equal(off.cpu().numpy(), want, err_msg="unaligned %s %s" % (layout, dt))
+            np.testing.assert_array_equal(_host(off), want, err_msg="unaligned %s %s" % (layout, dt))
     np.testing.assert_array_equal(env.legal_actions().cpu().numpy(),
                                   _obs_np(n, b, m, lg, "legal").reshape(E, n * n).astype(bool))
 
@@ -651,8 +662,9 @@ def test_observation_kernels_at_size(torch_cuda, n, E):
     env = make_env(torch, E, n, auto=True, seed=8)
     env.step_policy("random", n_plies=n * n // 2 + 1, record=False)
     b, m, lg = get_state_np(env)
-    for layout, dt in (("board", torch.int64), ("make_state", torch.float32), ("legal", torch.int8)):
-        np.testing.assert_array_equal(env.observe(layout, dt).cpu().numpy(), _obs_np(n, b, m, lg, layout),
+    for layout, dt in (("board", torch.int64), ("make_state", torch.float32), ("legal", torch.int8),
+                       ("make_state", torch.int8), ("make_state", torch.bfloat16)):
+        np.testing.assert_array_equal(_host(env.observe(layout, dt)), _obs_np(n, b, m, lg, layout),
                                       err_msg="%s %s" % (layout, dt))
 
 
@@ -667,8 +679,8 @@ def test_observation_large_launches_every_layout_and_dtype(torch_cuda, n, E):
     b, m, lg = get_state_np(env)
     for layout in ("board", "board_legal", "make_state", "absolute", "legal"):
         want = _obs_np(n, b, m, lg, layout)
-        for dt in (torch.int8, torch.int32, torch.int64, torch.float32, torch.float64):
-            got = env.observe(layout, dt).cpu().numpy()
+        for dt in (torch.int8, torch.int32, torch.int64, torch.float32, torch.float64, torch.bfloat16):
+            got = _host(env.observe(layout, dt))
             np.testing.assert_array_equal(got, want.astype(got.dtype), err_msg="%s %s" % (layout, dt))
 
 

@@ -23,7 +23,18 @@ def torch_cuda():
 
 
 def _dtypes(torch):
-    return (torch.int8, torch.int32, torch.int64, torch.float32, torch.float64)
+    return (torch.int8, torch.int32, torch.int64, torch.float32, torch.float64, torch.bfloat16)
+
+
+def host(o):
+    """An observation on the host as numpy (bfloat16, which numpy lacks, as
+    float32: -1 / 0 / +1 are exact in both); bfloat16's bit patterns checked."""
+    import torch
+    if o.dtype == torch.bfloat16:
+        bits = o.view(torch.int16).cpu().numpy()
+        assert np.isin(bits, [0, 0x3F80, 0xBF80 - 0x10000]).all(), "bfloat16 -1 / 0 / +1 bit patterns"
+        return o.float().cpu().numpy()
+    return o.cpu().numpy()
 
 
 def make_env(E, n, sd=True, auto=True, seed=9, init_rand=0):
@@ -94,8 +105,8 @@ def test_step_observe_every_layout_and_dtype(torch_cuda, n, E):
             np.testing.assert_array_equal(rew.cpu().numpy(), orw, err_msg=what)
             np.testing.assert_array_equal(dn.cpu().numpy(), od.astype(bool), err_msg=what)
             assert obs.dtype == dt
-            np.testing.assert_array_equal(obs.cpu().numpy(), oracle_obs(s, layout).astype(obs.cpu().numpy().dtype),
-                                          err_msg=what)
+            h = host(obs)
+            np.testing.assert_array_equal(h, oracle_obs(s, layout).astype(h.dtype), err_msg=what)
         b, m, lg = state_np(env)
         np.testing.assert_array_equal(b, s.boards)
         np.testing.assert_array_equal(m, s.meta)
@@ -197,6 +208,8 @@ def test_step_observe_on_terminated_boards(torch_cuda, n):
 
 
 @pytest.mark.parametrize("n,E,lay,dt", [(8, 65536, "make_state", "float32"), (8, 4096, "make_state", "float32"),
+                                        (8, 65536, "make_state", "int8"), (8, 65536, "make_state", "bfloat16"),
+                                        (8, 16384, "make_state", "bfloat16"), (6, 20000, "make_state", "int8"),
                                         (8, 70001, "board", "int64"), (6, 20000, "make_state", "float64"),
                                         (10, 5000, "board_legal", "int8"), (7, 3001, "make_state", "float32"),
                                         (12, 999, "board", "int32")])
@@ -226,8 +239,8 @@ def test_sample_step_observe(torch_cuda, n, E, lay, dt):
         assert o1.dtype == dtype and torch.equal(o1, o2), what + ": observation"
         orw, od, _ = oracle.step(s, oracle.F_SUDDEN_DEATH | oracle.F_AUTO_RESET, a1.cpu().numpy(), seed=3, ply=k)
         np.testing.assert_array_equal(r1.cpu().numpy(), orw, err_msg=what)
-        np.testing.assert_array_equal(o1.cpu().numpy(), oracle_obs(s, lay).astype(o1.cpu().numpy().dtype),
-                                      err_msg=what)
+        h = host(o1)
+        np.testing.assert_array_equal(h, oracle_obs(s, lay).astype(h.dtype), err_msg=what)
     for x, y in zip(fused.get_state(), split.get_state()):
         assert torch.equal(x, y)
     assert torch.equal(fused.counts(), split.counts())  # the per-wave W/D/L slots
@@ -285,7 +298,7 @@ def test_step_vs_observe_equals_two_calls(torch_cuda, n, opp, E):
     assert torch.equal(o1, o2)
     for c in range(12):
         acts = fused.policy_actions("greedy")
-        lay, dt = LAYOUTS[c % len(LAYOUTS)], _dtypes(torch)[c % 5]
+        lay, dt = LAYOUTS[c % len(LAYOUTS)], _dtypes(torch)[c % 6]
         o1, r1, d1, p1 = fused.step_vs(acts, opp, obs_layout=lay, obs_dtype=dt)
         _, r2, d2, p2 = split.step_vs(acts, opp, observe=False)
         o2 = split.observe(lay, dt)

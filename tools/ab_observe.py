@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--no-check", action="store_true", help="time variants that write other values (probes)")
     ap.add_argument("--layouts", default="board,make_state")
+    ap.add_argument("--dtype", help="one element type for every layout (default: board int64, make_state float32)")
     a = ap.parse_args()
     import torch
 
@@ -46,9 +47,10 @@ def main():
             env.step_policy("random", n_plies=25, record=False)
         forms = {"board": torch.int64, "make_state": torch.float32}
         for layout in a.layouts.split(","):
-            dt = forms[layout]
+            dt = getattr(torch, a.dtype) if a.dtype else forms.get(layout, torch.int8)
             esize = torch.empty(0, dtype=dt).element_size()
-            shape = (E, n, n) if layout == "board" else (E, 4, n, n)
+            shape = (E, n, n) if layout in ("board", "legal", "absolute") else \
+                ((E, 2, n, n) if layout == "board_legal" else (E, 4, n, n))
             bufs = {nm: torch.empty(shape, dtype=dt, device=dev) for nm in a.names}
             ref = None
             for nm, env in envs.items():
