@@ -1012,6 +1012,7 @@ struct NoFill {
     __device__ __forceinline__ void operator()() const {}
 };
 
+
 // black wins / draws / white wins from play_rand_fast's (sum of black's signs, games, decided games)
 __device__ __forceinline__ void tally_from_signs(uint32_t s, uint32_t g, uint32_t z, uint32_t& cb, uint32_t& cd,
                                                  uint32_t& cw) {
@@ -1039,8 +1040,13 @@ __device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_
         a = pick(u);  // RandomPolicy (simple_policies.py:37-41); L != 0
     } else if constexpr (OPEN) {
         // a random-opening ply draws u = action_draw(seed, id, g), from the caller's block
-        if (meta & 0xff00u) a = pick(u);
-        else a = OneWord<N>::greedy(eng.t, L);
+        // both computed and selected: as two exec-masked branches the wave ran both on
+        // most plies (some board of the 64 in its opening) with the pick's LDS round
+        // trip exposed between them; selected, the greedy planes' independent work
+        // hides it: config 3 at 65,536 boards 1.378 -> 1.318 us per ply (100-ply
+        // launches), 1.744 -> 1.697 (10-ply; profiles/r06/f)
+        const int ap = pick(u), ag = OneWord<N>::greedy(eng.t, L);
+        a = (meta & 0xff00u) ? ap : ag;
     } else {
         a = OneWord<N>::greedy(eng.t, L);
     }
