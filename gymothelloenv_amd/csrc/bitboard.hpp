@@ -1258,7 +1258,16 @@ OTH_HD U4 philox4(uint64_t seed, uint32_t id, uint64_t ctr, uint32_t purpose) {
 OTH_HD uint32_t philox_x(uint64_t seed, uint32_t id, uint64_t ply, uint32_t purpose) {
     return philox4(seed, id, ply, purpose).x;
 }
-OTH_HD uint32_t pick4(const U4& u, uint32_t j) { return j == 0 ? u.x : (j == 1 ? u.y : (j == 2 ? u.z : u.w)); }
+OTH_HD uint32_t pick4(const U4& u, uint32_t j) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    // by masks: on a wave-uniform j (a ply counter) the select chain became a tree
+    // of scalar branches, ~40-80 cycles each to a lone wave
+    const uint32_t m0 = 0u - (uint32_t)(j == 0), m1 = 0u - (uint32_t)(j == 1), m2 = 0u - (uint32_t)(j == 2);
+    return (u.x & m0) | (u.y & m1) | (u.z & m2) | (u.w & ~(m0 | m1 | m2));
+#else
+    return j == 0 ? u.x : (j == 1 ? u.y : (j == 2 ? u.z : u.w));
+#endif
+}
 // The random-move draw of ply g: word g % 4 of the block counter g / 4, so one
 // Philox evaluation serves four consecutive plies of a board.
 OTH_HD uint32_t action_draw(uint64_t seed, uint32_t id, uint64_t g) {

@@ -1236,23 +1236,31 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
         if constexpr (POLICY != OTH_POLICY_RANDOM) {  // scripted policy: draws only on opening plies
             if constexpr (OPEN) {
                 // an opening ply's draw is word g % 4 of Philox block g / 4 (action_draw's
-                // value); the block is computed once per group of four plies, at the first
-                // ply where some board of the wave has opening plies left (uniform branch):
-                // one Philox evaluation per 4 plies instead of one per ply.  The same for
-                // the auto-reset's opening-length draw (a wave-wide block per group, the
-                // draw spec changed to block form) measured 3-4 % slower: a wave's greedy
-                // games run almost in step, so few plies see a game end
-                // (profiles/r04/oblk/)
-                U4 blk{0u, 0u, 0u, 0u};
-                uint64_t held = ~0ull;  // the block in blk (wave-uniform)
-                for (int p = 0; p < plies; ++p) {
-                    const uint64_t g = ply0 + (uint64_t)p;
-                    if ((g >> 2) != held && __any((mt & 0xff00u) != 0)) {
-                        blk = philox4(rng.seed, id, g >> 2, RNG_ACTION);
-                        held = g >> 2;
-                    }
-                    ply(p, pick4(blk, (uint32_t)(g & 3)), nofill);
+                // value).  Plies in groups of four from a multiple of 4, as random play
+                // does: the group's block computed at its start and its words taken
+                // statically, instead of a per-ply test for a new block and a per-ply
+                // word choice (both scalar branches, ~40-80 cycles each to a lone wave):
+                // config 3 at 65,536 boards, 100-ply launches 1.315 -> 1.256-1.263 us per
+                // ply (profiles/r06/j, k).  (The auto-reset's opening-length draw in block form
+                // measured 3-4 % slower: a wave's greedy games run almost in step, so
+                // few plies see a game end, profiles/r04/oblk/.)
+                int p = 0;
+                // plies [p, q) inside one group: its block once, the words by pick4
+                auto partial = [&](int q) __attribute__((always_inline)) {
+                    const U4 blk = philox4(rng.seed, id, (ply0 + (uint64_t)p) >> 2, RNG_ACTION);
+                    for (; p < q; ++p) ply(p, pick4(blk, (uint32_t)((ply0 + (uint64_t)p) & 3)), nofill);
+                };
+                const int head = (int)((4u - (uint32_t)(ply0 & 3)) & 3u);
+                if (head > 0) partial(head < plies ? head : plies);
+                while (p + 4 <= plies) {
+                    const U4 blk = philox4(rng.seed, id, (ply0 + (uint64_t)p) >> 2, RNG_ACTION);
+                    ply(p, blk.x, nofill);
+                    ply(p + 1, blk.y, nofill);
+                    ply(p + 2, blk.z, nofill);
+                    ply(p + 3, blk.w, nofill);
+                    p += 4;
                 }
+                if (p < plies) partial(plies);
             } else {
                 for (int p = 0; p < plies; ++p) ply(p, 0u, nofill);
             }
