@@ -47,6 +47,10 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # VALU issue peak: 256 CUs x 4 SIMDs x one wave64 instruction per 2 cycles at 2.4 GHz
 VALU_PEAK_WAVE_INSTS = 256 * 4 * 2.4e9 / 2
+# ...and the ceiling with ONE wave per SIMD (65,536 boards = 1,024 waves on 1,024 SIMDs): a
+# lone wave issues at most one VALU instruction per 4 cycles (tools/ubench_valu3.hip,
+# profiles/r06/h; the play kernels' SQ_ACTIVE_INST_VALU / SQ_INSTS_VALU = 4.0)
+VALU_LONE_WAVE_CYCLES = 4.0
 METRIC = "env-steps/sec (random policy, 65,536×8×8 boards) at 1/2/4/8 GPUs; HBM GB/s vs peak"
 CONFIG2_BOARDS = 65536
 CONFIG4_BOARDS_PER_GPU = 131072
@@ -426,8 +430,14 @@ def make_record(args, world, G, E, P, n, record, wall_max, kern_ms, wdl_total, s
     valu = None
     if pmc and pmc.get("valu_insts_per_launch") and avg_launch_s:
         rate = pmc["valu_insts_per_launch"] / avg_launch_s
+        waves = -(-E // 64)
+        lone = None
+        if waves <= 1024:  # at most one wave per SIMD: the lone wave's issue interval bounds it
+            lone = waves * 2.4e9 / VALU_LONE_WAVE_CYCLES
         valu = {"achieved_wave_insts_per_s": rate, "peak_wave_insts_per_s": VALU_PEAK_WAVE_INSTS,
                 "frac": rate / VALU_PEAK_WAVE_INSTS,
+                "lone_wave_peak_wave_insts_per_s": lone,
+                "lone_wave_frac": rate / lone if lone else None,
                 # SQ_INSTS_VALU counts wave-instructions, each serving 64 boards: x 64 / board-plies
                 # is the length of one board's (one lane's) VALU instruction stream per ply
                 "valu_insts_per_board_ply": pmc["valu_insts_per_launch"] * 64 / (E * P),
@@ -729,7 +739,8 @@ def side_summary(side, out):
                                                                  "effective_clock_ghz")}
     v = (out.get("roofline") or {}).get("valu") or {}
     summ["headline"] = {"us_per_launch": _r(out["roofline"]["avg_launch_us"]), "frac": _r(out["roofline"]["frac"]),
-                        "valu_per_board_ply": _r(v.get("valu_insts_per_board_ply"))}
+                        "valu_per_board_ply": _r(v.get("valu_insts_per_board_ply")),
+                        "valu_lone_wave_frac": _r(v.get("lone_wave_frac"))}
     return summ
 
 
