@@ -1013,6 +1013,15 @@ struct NoFill {
 };
 
 
+// the terminal ply's reward: the disk difference (disk_reward, othello.py:446-459)
+// or the sign.  By a mask on the uniform flag: as `if (flags & ...)` the backend
+// made a scalar branch of it inside the terminal block (multi-word play: one per
+// ply the block runs, ~40-80 cycles to a lone wave)
+__device__ __forceinline__ int term_reward(uint32_t flags, int disk, int sg) {
+    const uint32_t m = 0u - (uint32_t)((flags & OTH_DISK_REWARD) != 0u);
+    return (int)__builtin_amdgcn_bitop3_b32(m, (uint32_t)disk, (uint32_t)sg, 0xCA);
+}
+
 // black wins / draws / white wins from play_rand_fast's (sum of black's signs, games, decided games)
 __device__ __forceinline__ void tally_from_signs(uint32_t s, uint32_t g, uint32_t z, uint32_t& cb, uint32_t& cd,
                                                  uint32_t& cw) {
@@ -1101,8 +1110,7 @@ __device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_
         if (term) {
             const int pc = popc64(Mn), oc = popc64(On), df = pc - oc;
             const int sg = sign_i32(df);  // the mover's result
-            if (flags & OTH_DISK_REWARD) r = oc == 0 ? NN : df;  // :446-459
-            else r = sg;                                           // winner * player_turn
+            r = term_reward(flags, oc == 0 ? NN : df, sg);  // :446-459 / winner * player_turn
             // the tally as (cb, cd, cw) = (sum of black's signs, games, decided games),
             // turned into wins / draws / wins by tally_from_signs: three adds, no selects
             const int mw = -(int)(mover & M_TURN_WHITE);  // 0 black, -1 white
@@ -1143,8 +1151,7 @@ __device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_
         if (term) {
             const int pc = popc64(Mn), oc = popc64(On), df = pc - oc;
             const int sg = sign_i32(df);  // the mover's result
-            if (flags & OTH_DISK_REWARD) r = oc == 0 ? NN : df;  // :446-459
-            else r = sg;                                           // winner * player_turn
+            r = term_reward(flags, oc == 0 ? NN : df, sg);  // :446-459 / winner * player_turn
             // the tally as (cb, cd, cw) = (sum of black's signs, games, decided games),
             // turned into wins / draws / wins by tally_from_signs: three adds, no selects
             const int m = -(int)(meta & M_TURN_WHITE);  // the mover (the turn is not passed on): 0 black, -1 white
@@ -1340,7 +1347,7 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand(uint64_t* __restrict__ boar
 // play_rand_fast for multi-word boards (N >= 9, the FillsW engine): the same
 // (mover, opponent) form with BB<W> words; every multi-word select is word by
 // word (a selected member address puts the lane in scratch).
-template <int N, typename FILL = NoFill>
+template <int N, bool OPEN = true, typename FILL = NoFill>
 __device__ __forceinline__ void play_rand_fast_w(BB<Geo<N>::W>& M, BB<Geo<N>::W>& O, BB<Geo<N>::W>& L,
                                                  uint32_t& meta, const FillsW<N>& eng, uint32_t u, uint32_t flags,
                                                  const Rng& rng, uint32_t id, uint64_t g, int& a, int& r, int& d,
@@ -1349,7 +1356,7 @@ __device__ __forceinline__ void play_rand_fast_w(BB<Geo<N>::W>& M, BB<Geo<N>::W>
     constexpr int W = Geo<N>::W;
     constexpr int NN = N * N;
     a = select_bit_tab(L, scale_index(u, popcount(L)), sel8);  // RandomPolicy (simple_policies.py:37-41); L != 0
-    meta -= (meta & 0xff00u) ? (1u << M_RAND_SHIFT) : 0u;
+    if constexpr (OPEN) meta -= (meta & 0xff00u) ? (1u << M_RAND_SHIFT) : 0u;
     const BB<W> m = square<W>(a);
     const BB<W> f = eng.flip(M, O, a);  // update_board (othello.py:391-410)
     const BB<W> Mn = M | f | m, On = O & ~f;
@@ -1388,16 +1395,17 @@ __device__ __forceinline__ void play_rand_fast_w(BB<Geo<N>::W>& M, BB<Geo<N>::W>
     if (term) {
         const int pc = popcount(Mn), oc = popcount(On), df = pc - oc;
         const int sg = sign_i32(df);  // the mover's result
-        if (flags & OTH_DISK_REWARD) r = oc == 0 ? NN : df;  // :446-459
-        else r = sg;
+        r = term_reward(flags, oc == 0 ? NN : df, sg);  // :446-459 / winner * player_turn
         const int mw = -(int)(mover & M_TURN_WHITE);  // (cb, cd, cw) as in play_rand_fast
         const int sb = (sg ^ mw) - mw;
         cb += (uint32_t)sb;
         cd += 1u;
         cw += (uint32_t)__mul24(sb, sb);
         uint32_t rl = 0;
-        if (rng.init_rand > 0)
-            rl = (uint32_t)scale_index(philox_x(rng.seed, id, g, RNG_OPENING_AUTO), rng.init_rand / 2 + 1) * 2u;
+        if constexpr (OPEN) {  // (without: no opening plies and none drawn, the scalar branch compiled out)
+            if (rng.init_rand > 0)
+                rl = (uint32_t)scale_index(philox_x(rng.seed, id, g, RNG_OPENING_AUTO), rng.init_rand / 2 + 1) * 2u;
+        }
         meta = (rl & 0xffu) << M_RAND_SHIFT;
     }
 }
@@ -1438,17 +1446,20 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand_w(uint64_t* __restrict__ bo
         int32_t* rew_p = rewards + e;
         uint8_t* done_p = dones + e;
         uint32_t t0 = 0, t1 = 0, t2 = 0;  // play_rand_fast_w's tally (tally_from_signs)
-        auto ply = [&](uint64_t g, uint32_t u, const auto& fill) __attribute__((always_inline)) {
-            int a, r, d;
-            play_rand_fast_w<N>(M, O, L, mt, eng, u, flags, rng, id, g, a, r, d, t0, t1, t2, sel8, fill);
-            *act_p = a;
-            *rew_p = r;
-            *done_p = (uint8_t)d;
-            act_p += E;
-            rew_p += E;
-            done_p += E;
-        };
-        if (!slow) {
+        // OPEN: some board of the wave may have or draw random-opening plies; without,
+        // the opening bookkeeping and the reset's opening draw are compiled out
+        auto fast = [&](auto OPENC) __attribute__((always_inline)) {
+            constexpr bool OPEN = decltype(OPENC)::value;
+            auto ply = [&](uint64_t g, uint32_t u, const auto& fill) __attribute__((always_inline)) {
+                int a, r, d;
+                play_rand_fast_w<N, OPEN>(M, O, L, mt, eng, u, flags, rng, id, g, a, r, d, t0, t1, t2, sel8, fill);
+                *act_p = a;
+                *rew_p = r;
+                *done_p = (uint8_t)d;
+                act_p += E;
+                rew_p += E;
+                done_p += E;
+            };
             // Philox block g/4 serves plies 4k..4k+3 (g uniform: scalar branches).
             // Two-word boards compute the next block in the current group's first ply
             // (as k_play_rand: 10x10 +5 %); boards of 3+ words, already past 256 VGPRs,
@@ -1498,6 +1509,11 @@ __global__ __launch_bounds__(BLOCK) void k_play_rand_w(uint64_t* __restrict__ bo
                     ++p;
                 }
             }
+        };
+        if (!slow) {
+            // (one loop for both: 10x10 without openings 1.422 -> 1.447 us per ply, profiles/r06/n)
+            if (rng.init_rand == 0 && !__any((mt & 0xff00u) != 0)) fast(std::false_type{});
+            else fast(std::true_type{});
             tally_from_signs(t0, t1, t2, cb, cd, cw);
             const bool tw = (mt & M_TURN_WHITE) != 0;
 #pragma unroll
