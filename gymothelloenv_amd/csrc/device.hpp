@@ -299,15 +299,28 @@ struct Fills {
         r.w[0] = OneWord<N>::legal(Pb.w[0], Ob.w[0], t);
         return r;
     }
+    // FIRST: the eight ray loads issued together before the runs (a scheduling
+    // barrier after them), one LDS round trip instead of the two the backend's
+    // interleaving left: greedy 100-ply launches 1.296 -> 1.264 us per ply, 6x6
+    // random 0.791 -> 0.775, but 8x8 random 0.685 -> 0.689 (profiles/r06/t, u),
+    // so k_play_rand asks for it except at 8x8 random play
+    template <bool FIRST = false>
     __device__ __forceinline__ BB<1> flip(const BB<1>&, const BB<1>&, int a) const {
         const uint64_t* r = rays + a;
         // (the rays computed by RayMath instead of read from the LDS table: 8x8
         // 0.671 -> 0.696 us per ply, greedy +2.8 %, 6x6 +3.3 %: +38 VALU per ply cost
         // more than the LDS round trip they remove; profiles/r04/fm/ab.jsonl)
+        uint64_t rr[8];
+        if constexpr (FIRST) {
+#pragma unroll
+            for (int d = 0; d < 8; ++d) rr[d] = r[64 * d];
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        auto ray_of = [&](int d) __attribute__((always_inline)) { return FIRST ? rr[d] : r[64 * d]; };
         uint64_t f = 0;
 #pragma unroll
         for (int d = 0; d < 4; ++d) {  // toward higher squares: cap = lowest ray square outside the fill
-            const uint64_t ray = r[64 * d];
+            const uint64_t ray = ray_of(d);
             const uint64_t y = ray & ~t[d];
             // ray & ((y & -y) - 1) == ray & t & (y - 1): one 3-input AND per dword
             f |= and3_64(ray, t[d], y - 1ull);
@@ -320,7 +333,7 @@ struct Fills {
         uint64_t g = 0;
 #pragma unroll
         for (int d = 4; d < 8; ++d) {
-            const uint64_t ray = r[64 * d];
+            const uint64_t ray = ray_of(d);
             const uint64_t tt = OneWord<N>::turn180(t[d]);
             const uint64_t y = ray & ~tt;
             g |= and3_64(ray, tt, y - 1ull);
@@ -1063,7 +1076,10 @@ __device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_
     const uint64_t m = 1ull << a;
     BB<1> dummy;
     dummy.w[0] = 0;
-    const uint64_t f = eng.flip(dummy, dummy, a).w[0];  // update_board (othello.py:391-410)
+    constexpr bool RAYS_FIRST = POLICY != OTH_POLICY_RANDOM || N != 8;
+    uint64_t f;  // update_board (othello.py:391-410)
+    if constexpr (std::is_same<Eng, Fills<N>>::value) f = eng.template flip<RAYS_FIRST>(dummy, dummy, a).w[0];
+    else f = eng.flip(dummy, dummy, a).w[0];
     const uint64_t Mn = M | f | m, On = O & ~f;
     const bool full = (Mn | On) == BD;  // :425-426
     if constexpr (POLICY == OTH_POLICY_RANDOM) {
