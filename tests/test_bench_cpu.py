@@ -41,7 +41,7 @@ def test_plan_defaults_per_config():
         bench.plan(bench.parse_args(["--envs", "5", "--global-envs", "10"]), 1, 0)
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_spawned_ranks_cover_the_global_boards(world):
     """--gpus N without WORLD_SIZE: bench.py starts N ranks (RANK/LOCAL_RANK/
     WORLD_SIZE set), they form a gloo group and all-gather their shard plans."""
@@ -64,6 +64,28 @@ def test_spawned_ranks_cover_the_global_boards(world):
         assert k in d, k
     assert d["n_gpus"] == world and d["ranks"] == world and d["shared_device"] is False
     assert d["config"]["boards_per_gpu"] == 131072 and d["roofline"]["bound"] == "valu-issue"
+
+
+def test_driver_torchrun_launch_of_eight_ranks():
+    """The driver's own N = 8 command (torch.distributed.run, one rank per GPU,
+    127.0.0.1 rendezvous) as a dry run on CPU ranks: the launch, the WORLD_SIZE
+    check, the shard plan of config 4 and rank 0's single JSON line."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port),
+                        os.path.join(ROOT, "bench.py"), "--gpus", "8", "--dry-run"],
+                       env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(line) == 1, r.stdout
+    d = json.loads(line[0])
+    assert d["world"] == 8 and d["n_gpus"] == 8 and d["global_envs"] == 1048576
+    assert sorted(d["shards"]) == [[k, k * 131072, 131072] for k in range(8)]
+    assert d["config"]["boards_per_gpu"] == 131072 and d["scaling"] == "weak"
 
 
 def test_shared_device_rehearsal_is_labelled():
