@@ -14,6 +14,10 @@
 #include <stdint.h>
 #include <type_traits>
 
+#ifndef OTH_OPENING_PHILOX
+#define OTH_OPENING_PHILOX 0  // opening-length draws by Philox (round-5 spec; A/B timing arm, round 6)
+#endif
+
 #if defined(__HIPCC__)
 #define OTH_HD __host__ __device__ __forceinline__
 #else
@@ -1257,6 +1261,34 @@ OTH_HD U4 philox4(uint64_t seed, uint32_t id, uint64_t ctr, uint32_t purpose) {
 }
 OTH_HD uint32_t philox_x(uint64_t seed, uint32_t id, uint64_t ply, uint32_t purpose) {
     return philox4(seed, id, ply, purpose).x;
+}
+// The random-opening length draw (SimpleOthelloEnv.reset's randint, othello.py:62-63,
+// at a reset or an auto-reset): one 32-bit word from (seed, env id, ply, purpose) by
+// murmur3's 32-bit finaliser: a key from the seed and the purpose, then the ply (both
+// wave-uniform: scalar work), then the env id: 5-7 VALU a lane, where a Philox4x32-10
+// evaluation was ~40 with 16-19 v_mad_u64_u32.  The terminal block that draws it runs
+// on most of a wave's plies (some board of 64 ends a game): config 3 at 65,536 boards,
+// 100-ply launches -3.9 % with a cheap draw in its place (profiles/r06/aa).  A choice
+// among init_rand / 2 + 1 <= 6 lengths needs the top bits well mixed, which fmix32's
+// avalanche gives; the action and sampling draws stay Philox.
+OTH_HD uint32_t fmix32(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    h *= 0xC2B2AE35u;
+    h ^= h >> 16;
+    return h;
+}
+OTH_HD uint32_t opening_draw(uint64_t seed, uint32_t id, uint64_t ply, uint32_t purpose) {
+#if OTH_OPENING_PHILOX  // A/B timing arm only (other values: the oracle follows the hash)
+    return philox_x(seed, id, ply, purpose);
+#else
+    // the key depends on the seed and the purpose alone (loop-invariant: hoisted out
+    // of the play loops), the ply enters once, the env id last
+    const uint32_t key = fmix32((uint32_t)seed ^ fmix32((uint32_t)(seed >> 32) ^ purpose * 0x7FEB352Du));
+    const uint32_t c = fmix32(key ^ (uint32_t)ply ^ (uint32_t)(ply >> 32) * 0x9E3779B9u);
+    return fmix32(c ^ id);
+#endif
 }
 OTH_HD uint32_t pick4(const U4& u, uint32_t j) {
 #if defined(__HIP_DEVICE_COMPILE__)

@@ -487,7 +487,7 @@ __device__ __forceinline__ void reset_lane(Lane<N>& s, uint64_t seed, uint32_t i
     s.white = Start<N>::WHITE;
     s.legal = legal_moves<N>(s.black, s.white);  // black moves first (othello.py:267)
     uint32_t rl = 0;
-    if (init_rand > 0) rl = (uint32_t)scale_index(philox_x(seed, id, ply, purpose), init_rand / 2 + 1) * 2u;
+    if (init_rand > 0) rl = (uint32_t)scale_index(opening_draw(seed, id, ply, purpose), init_rand / 2 + 1) * 2u;
     s.meta = (rl & 0xffu) << M_RAND_SHIFT;
 }
 
@@ -1136,7 +1136,7 @@ __device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_
             cw += (uint32_t)__mul24(sb, sb);
             uint32_t rl = 0;
             if (rng.init_rand > 0)
-                rl = (uint32_t)scale_index(philox_x(rng.seed, id, g, RNG_OPENING_AUTO), rng.init_rand / 2 + 1) * 2u;
+                rl = (uint32_t)scale_index(opening_draw(rng.seed, id, g, RNG_OPENING_AUTO), rng.init_rand / 2 + 1) * 2u;
             meta = (rl & 0xffu) << M_RAND_SHIFT;
         }
     } else {
@@ -1185,7 +1185,7 @@ __device__ __forceinline__ void play_rand_fast(uint64_t& M, uint64_t& O, uint64_
             for (int k = 0; k < 8; ++k) eng.t[k] = SF.t[k];
             uint32_t rl = 0;
             if (rng.init_rand > 0)
-                rl = (uint32_t)scale_index(philox_x(rng.seed, id, g, RNG_OPENING_AUTO), rng.init_rand / 2 + 1) * 2u;
+                rl = (uint32_t)scale_index(opening_draw(rng.seed, id, g, RNG_OPENING_AUTO), rng.init_rand / 2 + 1) * 2u;
             meta = (rl & 0xffu) << M_RAND_SHIFT;
         }
     }
@@ -1420,7 +1420,7 @@ __device__ __forceinline__ void play_rand_fast_w(BB<Geo<N>::W>& M, BB<Geo<N>::W>
         uint32_t rl = 0;
         if constexpr (OPEN) {  // (without: no opening plies and none drawn, the scalar branch compiled out)
             if (rng.init_rand > 0)
-                rl = (uint32_t)scale_index(philox_x(rng.seed, id, g, RNG_OPENING_AUTO), rng.init_rand / 2 + 1) * 2u;
+                rl = (uint32_t)scale_index(opening_draw(rng.seed, id, g, RNG_OPENING_AUTO), rng.init_rand / 2 + 1) * 2u;
         }
         meta = (rl & 0xffu) << M_RAND_SHIFT;
     }

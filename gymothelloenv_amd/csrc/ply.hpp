@@ -301,7 +301,7 @@ __device__ __forceinline__ void ply_body(uint64_t* __restrict__ boards, uint16_t
         L = START_MOVES;
         uint32_t rl = 0;
         if (rng.init_rand > 0)
-            rl = (uint32_t)scale_index(philox_x(rng.seed, id, ply, RNG_OPENING_AUTO), rng.init_rand / 2 + 1) * 2u;
+            rl = (uint32_t)scale_index(opening_draw(rng.seed, id, ply, RNG_OPENING_AUTO), rng.init_rand / 2 + 1) * 2u;
         m = (rl & 0xffu) << M_RAND_SHIFT;
     }
     if (mine) {
@@ -419,7 +419,7 @@ __global__ __launch_bounds__(BLOCK) void k_ply_step_obs(uint64_t* __restrict__ b
         L = START_MOVES;
         uint32_t rl = 0;
         if (rng.init_rand > 0)
-            rl = (uint32_t)scale_index(philox_x(rng.seed, id, ply, RNG_OPENING_AUTO), rng.init_rand / 2 + 1) * 2u;
+            rl = (uint32_t)scale_index(opening_draw(rng.seed, id, ply, RNG_OPENING_AUTO), rng.init_rand / 2 + 1) * 2u;
         m = (rl & 0xffu) << M_RAND_SHIFT;
     }
     if (mine && h == 0) {
@@ -561,7 +561,7 @@ __global__ __launch_bounds__(BLOCK) void k_step_vs1(uint64_t* __restrict__ board
                     L = START_MOVES;
                     uint32_t rl = 0;
                     if (rng.init_rand > 0)
-                        rl = (uint32_t)scale_index(philox_x(rng.seed, id, call, RNG_OPENING_AUTO),
+                        rl = (uint32_t)scale_index(opening_draw(rng.seed, id, call, RNG_OPENING_AUTO),
                                                    rng.init_rand / 2 + 1) * 2u;
                     m = (rl & 0xffu) << M_RAND_SHIFT;
                     if constexpr (KEEP) {  // the start position's fills (black to move)

@@ -243,11 +243,6 @@ static void philox(uint32_t key0, uint32_t key1, uint32_t c[4]) {
     }
 }
 
-static uint32_t draw(uint64_t seed, uint32_t env_id, uint64_t ply, uint32_t purpose) {
-    uint32_t c[4] = {env_id, (uint32_t)ply, (uint32_t)(ply >> 32), purpose};
-    philox((uint32_t)seed, (uint32_t)(seed >> 32), c);
-    return c[0];
-}
 
 /* ---------------- bitboard exchange ---------------- */
 static void load(oenv *e, int n, uint32_t flags, const uint64_t *bd, uint16_t meta, const uint64_t *lg) {
@@ -386,9 +381,26 @@ static int random_action(const oenv *e, uint64_t seed, uint32_t id, uint64_t ply
     return e->moves[k];
 }
 
+/* The opening-length word: murmur3's 32-bit finaliser on a key of (seed, purpose),
+ * then the ply, then the env id -- the device's opening_draw (bitboard.hpp). */
+static uint32_t fmix32(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    h *= 0xC2B2AE35u;
+    h ^= h >> 16;
+    return h;
+}
+static uint32_t opening_draw(uint64_t seed, uint32_t id, uint64_t ply, uint32_t purpose) {
+    uint32_t key = fmix32((uint32_t)seed ^ fmix32((uint32_t)(seed >> 32) ^ purpose * 0x7FEB352Du));
+    uint32_t c = fmix32(key ^ (uint32_t)ply ^ (uint32_t)(ply >> 32) * 0x9E3779B9u);
+    return fmix32(c ^ id);
+}
+
 static int opening_plies(uint64_t seed, uint32_t id, uint64_t ply, uint32_t purpose, int initial_rand_steps) {
-    /* SimpleOthelloEnv.reset: randint(0, k//2 + 1) * 2 (othello.py:62-63) */
-    uint32_t u = draw(seed, id, ply, purpose);
+    /* SimpleOthelloEnv.reset: randint(0, k//2 + 1) * 2 (othello.py:62-63), the word
+     * from opening_draw (Philox drew it up to round 5) */
+    uint32_t u = opening_draw(seed, id, ply, purpose);
     return (int)(((uint64_t)u * (uint64_t)(initial_rand_steps / 2 + 1)) >> 32) * 2;
 }
 
